@@ -1,0 +1,155 @@
+/*
+ * marlmaze.h -- C ABI of the MI355X (gfx950) MARL-Maze hot path.
+ *
+ * Library: marl-maze_amd/libmarlmaze.so (hipcc --offload-arch=gfx950).
+ *
+ * The reference (rhuangr/MARL-Maze) is pure Python and has no FFI; the entry
+ * points below are what its Python classes would bind to run the hot path on
+ * the GPU.  Each cites the reference interface it replaces:
+ *
+ *   mm_env_seed   random.seed(s) before Maze.reset()           (maze.py:170-259 draws
+ *                                                              from the global `random`)
+ *   mm_env_reset  Maze.reset()                                  maze.py:55-72
+ *   mm_env_step   Maze.step(action) (+ PPO.get_batch's reset     maze.py:74-163,
+ *                 on done, PPO.py:127-130)                      maze_agent.py:89-358
+ *   mm_gae        PPO.get_GAEs                                  PPO.py:193-203
+ *   mm_sample     PPO.get_action (masked Categorical move +     PPO.py:170-186
+ *                 Bernoulli mark, joint log-prob)
+ *
+ * Conventions
+ *   - Every pointer is a caller-owned DEVICE buffer (e.g. a torch tensor);
+ *     the library never allocates, frees or synchronises.  All work is
+ *     enqueued on `stream` (a hipStream_t passed as void*; NULL = default
+ *     stream) and is graph-capturable.
+ *   - Return value: 0 on success, otherwise a hipError_t from the launch or a
+ *     negative MM_E* code for invalid arguments.  Device-side failures (an
+ *     illegal move, a maze whose key cannot be placed: maze.py:254 loops
+ *     forever there) set bits in mm_maze_t.status instead.
+ *   - Layout bytes: bits 0-1 = the reference's cell value (0 path, 1 wall,
+ *     2/3 = mark of the agent with that tag, maze.py:133), bits 2-4 = the
+ *     direction of the next step toward the exit (0..3 = N,E,S,W as
+ *     maze.py:19 DELTAS; 4 = this is the exit).  The reference's per-agent
+ *     exit_route stack (maze.py:148-154) always equals the tree path, so the
+ *     table replaces it.
+ *   - Observation row = 65 f32 in Appendix-A order (maze_agent.py:89-130);
+ *     mask row = 6 bytes (0/1), maze_agent.py:132-139 + maze.py:107-113.
+ */
+#ifndef MARLMAZE_H
+#define MARLMAZE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MM_OBS_DIM 65
+#define MM_MASK_DIM 6
+#define MM_RNG_WORDS 625   /* CPython random.getstate()[1]: 624 words + index */
+#define MM_MAX_SIDE 41     /* layout side limit (default_size <= 21) */
+#define MM_MAZES_PER_BLOCK 64
+
+#define MM_E_ARG (-1)
+#define MM_E_SIZE (-2)
+
+/* mm_maze_t.status bits */
+#define MM_ST_GEN_FAIL 1u      /* set_key/set_end found no cell (reference hangs) */
+#define MM_ST_BAD_MOVE 2u      /* an action moved into a wall / off the grid */
+
+/* Per-agent state: 32 bytes (maze_agent.py:16-79). */
+typedef struct {
+    int8_t x, y, dir, flags;        /* flags: MM_AF_* */
+    int8_t lmx, lmy, olsx, olsy;    /* last_mark_pos, other_last_seen */
+    int8_t minx, maxx, miny, maxy;  /* *_visited (Q9) */
+    int8_t mem[4];                  /* deque(maxlen=4) of relative moves, -1 = empty */
+    int32_t exit_len;               /* maze_agent.py:33 */
+    int32_t tfls;                   /* time_from_last_seen, never reset (Q5) */
+    int32_t reserved[2];
+} mm_agent_t;
+
+#define MM_AF_KNOWS_END 1
+#define MM_AF_SEES_END 2
+#define MM_AF_OTHER_KNOWS 4
+#define MM_AF_HAS_KEY 8
+#define MM_AF_SEES_KEY 16
+#define MM_AF_TEAM_KEY 32
+#define MM_AF_HAS_MARK 64
+
+/* Per-maze scalars: 32 bytes (maze.py:22-53). */
+typedef struct {
+    int32_t t;            /* current_t */
+    int8_t w, h;          /* width, height (2*size-1) */
+    int8_t ex, ey;        /* end */
+    int8_t kx, ky;        /* key; kx = -1 after pickup (maze.py:157-158) */
+    int8_t sx, sy;        /* start */
+    int16_t path_len;     /* shortest_path_len */
+    uint16_t status;      /* MM_ST_* */
+    int32_t episodes;     /* completed episodes */
+    int32_t last_len;     /* length of the last completed episode */
+    int32_t last_path;    /* shortest_path_len of the last completed episode */
+    int32_t spawn1;       /* shortest_path[1] = agent 1's spawn, x | y << 8 (maze.py:66) */
+} mm_maze_t;
+
+/* Environment descriptor (host struct holding device pointers). */
+typedef struct {
+    int32_t n;                     /* number of mazes */
+    int32_t size_w, size_h;        /* default_size in cells (maze.py:23) */
+    int32_t max_timestep;          /* maze.py:22 */
+    int32_t difficulty;            /* maze.py:22 */
+    int32_t rand_start;            /* maze.py:22 */
+    int32_t rand_sizes;            /* maze.py:23 */
+    int32_t rand_lo, rand_hi;      /* rand_range */
+    int32_t layout_stride;         /* bytes per maze layout (>= side_max^2) */
+    uint8_t* layout;               /* [n, layout_stride] */
+    mm_agent_t* agents;            /* [n, 2] */
+    mm_maze_t* mazes;              /* [n] */
+    uint32_t* rng;                 /* [n, MM_RNG_WORDS] */
+    int32_t* work;                 /* [n + 64] scratch (done list) */
+} mm_env_t;
+
+/* Library version (major*100 + minor). */
+int mm_version(void);
+
+/* Bytes needed for layout_stride given the config (side_max^2). */
+int mm_layout_stride(int size_w, int size_h, int rand_sizes, int rand_lo, int rand_hi);
+
+/* random.seed(seeds[i]) for every maze i; also initialises the agents as
+ * Agent.__init__ does (x=y=0, facing south; maze_agent.py:24-57).
+ * seeds: device [n] uint64. */
+int mm_env_seed(const mm_env_t* env, const uint64_t* seeds, void* stream);
+
+/* Maze.reset() for the mazes with reset_mask[i] != 0 (reset_mask may be NULL
+ * = all).  Writes obs [n,2,65] f32 and masks [n,2,6] u8 rows of those mazes. */
+int mm_env_reset(const mm_env_t* env, const uint8_t* reset_mask, float* obs, uint8_t* masks, void* stream);
+
+/* Maze.step(actions) for every maze.  actions [n,2,2] int8 = (move, mark) per
+ * agent.  Outputs obs [n,2,65] f32, masks [n,2,6] u8, reward [n] f32,
+ * done [n] u8.  With auto_reset != 0 the finished mazes are regenerated and
+ * their obs/mask rows replaced by the reset observation (PPO.py:127-130). */
+int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward, uint8_t* done,
+                int auto_reset, void* stream);
+
+/* Time-major GAE over [T, N] (PPO.py:193-203, episodes concatenated in time,
+ * done[t] = the transition at t ended its episode).  last_value [N] (may be
+ * NULL): bootstrap for segments that end mid-episode; NULL makes every
+ * segment end an episode end (done[T-1] := 1: the reference's GAE applied
+ * to each episode fragment, PPO.py:197-198).
+ * gamma, gamma_lambda are the f32 factors (f32(0.99), f32(0.99*0.95)).
+ * adv, rtg = adv + value: [T, N] f32.  Arithmetic is fp32 with no FMA, in
+ * the reference's operation order: bit-exact. */
+int mm_gae(const float* reward, const float* value, const uint8_t* done, const float* last_value, int T, int N,
+           float gamma, float gamma_lambda, float* adv, float* rtg, void* stream);
+
+/* Sample one action per agent row (PPO.py:170-186): move ~ Categorical over
+ * move_logits [M,5] masked to -inf where masks[:,0:5]==0; mark ~ Bernoulli(
+ * sigmoid(mark_logit [M])) where masks[:,5] else 0.  Rows are (maze, agent)
+ * pairs: M = 2N.  actions [M,2] int8; logp [M] per-agent log-prob; joint_logp
+ * [N] = logp[2i] + logp[2i+1] (may be NULL).  Counter-based Philox4x32-10
+ * keyed by (seed), counter = (offset, row): reproducible and replayable. */
+int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M, uint64_t seed,
+              uint64_t offset, int8_t* actions, float* logp, float* joint_logp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MARLMAZE_H */

@@ -1,0 +1,494 @@
+// env_kernels.hip -- batched MARL-Maze environment on MI355X (gfx950).
+//
+// Kernels
+//   k_seed   one thread per maze: random.seed(seed_i) into the maze's
+//            CPython MT19937 row, Agent.__init__ state (maze_agent.py:24-57).
+//   k_reset  one 64-lane wavefront per maze: Maze.build_maze (maze.py:170-259):
+//            recursive-backtracker generation with the maze's own MT19937
+//            stream in LDS, plus the per-cell direction-to-exit table.
+//   k_reset_obs  one thread per reset maze: agent resets and the two reset
+//            observations in the reference's order (maze.py:64-71: agent 0
+//            observes while agent 1 still holds its previous state, Q3).
+//   k_step   one thread per maze, 64 mazes per workgroup: Maze.step()
+//            (maze.py:74-122).  The workgroup's 64 layouts are one
+//            contiguous HBM range and are staged into LDS with 16-byte
+//            coalesced loads; observations and masks are staged in LDS and
+//            written back as contiguous 16-byte stores.  Finished mazes are
+//            appended to a done list that k_reset consumes (PPO.py:127-130).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "env_device.h"
+#include "marlmaze.h"
+#include "mt19937_wave.h"
+
+extern "C" int mm_layout_stride(int size_w, int size_h, int rand_sizes, int rand_lo, int rand_hi);
+
+namespace mm {
+
+constexpr int kMPB = MM_MAZES_PER_BLOCK;  // mazes per step workgroup
+constexpr int kMaxCells = MM_MAX_SIDE * MM_MAX_SIDE;
+constexpr int kGenTries = 1 << 16;  // rejection-loop bound, same as oracle GEN_TRIES (reference: unbounded)
+constexpr int kListOff = 64;        // done list starts at work[64]
+
+// ---------------------------------------------------------------------------
+// cooperative contiguous copies (whole workgroup)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void copy_in(uint8_t* dst, const uint8_t* src, int bytes) {
+    const int nv = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (int k = threadIdx.x; k < nv; k += blockDim.x) d4[k] = s4[k];
+    for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) dst[k] = src[k];
+}
+
+__device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int bytes) {
+    const int nv = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (int k = threadIdx.x; k < nv; k += blockDim.x) d4[k] = s4[k];
+    for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) dst[k] = src[k];
+}
+
+// ---------------------------------------------------------------------------
+// seed
+// ---------------------------------------------------------------------------
+__global__ void k_seed(mm_env_t env, const uint64_t* __restrict__ seeds) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= env.n) return;
+    mt_seed_thread(env.rng + (size_t)m * MM_RNG_WORDS, seeds[m]);
+    for (int a = 0; a < 2; a++) {  // Agent.__init__ (maze_agent.py:24-57)
+        Agent g;
+        g.x = g.y = 0;
+        g.dir = 2;
+        g.flags = 0;
+        g.lmx = g.lmy = 0;
+        g.olsx = g.olsy = 0;
+        g.minx = g.maxx = g.miny = g.maxy = 0;
+        g.mem = 0xffffffffu;
+        g.exit_len = -1;
+        g.tfls = 0;
+        g.tag = 2 + a;
+        env.agents[2 * m + a] = pack_agent(g);
+    }
+    mm_maze_t z = {};
+    z.kx = z.ky = -1;
+    env.mazes[m] = z;
+}
+
+// ---------------------------------------------------------------------------
+// generation + reset (one wavefront per maze)
+// ---------------------------------------------------------------------------
+struct GenLds {
+    uint32_t mt[kMtN];
+    uint8_t cell[kMaxCells];     // layout being built (values 0/1)
+    uint8_t par[kMaxCells];      // direction toward the root (start); bit 7 = on start->end path
+    uint8_t pdir[kMaxCells];     // on-path cells: direction toward the end
+    int16_t depth[kMaxCells];    // tree depth from start
+    int16_t stack[kMaxCells];    // DFS stack (cell indices)
+};
+
+// Maze.build_maze + set_start/end/key (maze.py:170-259), wave-uniform.
+// Returns false if a rejection loop exhausted its bound (the reference would
+// loop forever).
+__device__ bool generate(const mm_env_t& env, GenLds& g, WaveRng& rng, int& w, int& h, int& sx, int& sy, int& ex,
+                         int& ey, int& kx, int& ky, int& plen, int& p1x, int& p1y) {
+    const int lane = threadIdx.x;
+    if (env.rand_sizes) {  // :171-174
+        const int s = rng.randint(env.rand_lo, env.rand_hi) * 2 - 1;
+        w = h = s;
+    } else {
+        w = env.size_w * 2 - 1;
+        h = env.size_h * 2 - 1;
+    }
+    const int nc = w * h;
+    for (int c = lane; c < nc; c += 64) {
+        g.cell[c] = 1;
+        g.par[c] = 0x7f;
+        g.depth[c] = 0;
+    }
+    if (env.rand_start) {  // set_start :229-237
+        sx = rng.randint(0, (w - 1) / 2) * 2;
+        sy = rng.randint(0, (h - 1) / 2) * 2;
+    } else {
+        sx = ((w / 2) % 2 == 0) ? w / 2 : w / 2 - 1;
+        sy = 0;
+    }
+    __syncthreads();
+    // recursive backtracker :180-201
+    int sp = 0;
+    const int s0 = sy * w + sx;
+    if (lane == 0) {
+        g.stack[0] = (int16_t)s0;
+        g.par[s0] = kDirNone;
+    }
+    sp = 1;
+    double corridor = 0.0;
+    const double inc = 1.0 / (10 * (w > h ? w : h));
+    __syncthreads();
+    while (sp > 0) {
+        const int c = g.stack[sp - 1];
+        const int cx = c % w, cy = c / w;
+        int nbd[4] = {0, 0, 0, 0};
+        int nn = 0;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {  // get_neighbors :220-227
+            const int nx = cx + 2 * ddx(d), ny = cy + 2 * ddy(d);
+            if (nx >= 0 && nx < w && ny >= 0 && ny < h && g.cell[ny * w + nx] == 1) nbd[nn++] = d;
+        }
+        // layout[cur] = 0 (cells are only ever carved, so writing after the
+        // neighbour scan is equivalent: the scan never looks at `c` itself)
+        if (lane == 0) g.cell[c] = 0;
+        if (nn && rng.random() > corridor) {
+            const int pick = rng.below((uint32_t)nn);
+            int d = nbd[0];
+#pragma unroll
+            for (int q = 1; q < 4; q++)
+                if (q == pick) d = nbd[q];
+            const int mx = cx + ddx(d), my = cy + ddy(d);
+            const int nx = mx + ddx(d), ny = my + ddy(d);
+            const int mi = my * w + mx, ni = ny * w + nx;
+            const int back = (d + 2) & 3;
+            if (lane == 0) {
+                g.cell[mi] = 0;
+                g.par[mi] = (uint8_t)back;
+                g.par[ni] = (uint8_t)back;
+                g.depth[mi] = (int16_t)(g.depth[c] + 1);
+                g.depth[ni] = (int16_t)(g.depth[c] + 2);
+                g.stack[sp] = (int16_t)ni;
+            }
+            sp++;
+            corridor += inc;
+        } else {
+            sp--;
+            corridor = 0.0;
+        }
+        __syncthreads();
+    }
+    // ends: difficulty x set_end, keep the longest (last of equal length) :204-217
+    int best = 0;
+    ex = ey = 0;
+    for (int r = 0; r < env.difficulty; r++) {
+        const int coin = rng.randint(0, 1);  // set_end :239-250
+        const int x = coin == 0 ? 0 : w - 1;
+        int y = -1;
+        for (int tries = 0; tries < kGenTries; tries++) {
+            const int yy = rng.randint(0, h - 1);
+            if (x == sx && yy == sy) continue;
+            if (g.cell[yy * w + x] == 0) {
+                y = yy;
+                break;
+            }
+        }
+        if (y < 0) {  // give up (the reference loops forever): end = start, path = [start], no key
+            ex = sx;
+            ey = sy;
+            plen = 1;
+            p1x = sx;
+            p1y = sy;
+            kx = ky = -1;
+            return false;
+        }
+        const int len = g.depth[y * w + x] + 1;  // len(get_shortest_path) in a tree
+        if (len > best) best = len;
+        if (len == best) {
+            ex = x;
+            ey = y;
+        }
+    }
+    plen = best;
+    // walk end -> start: mark the path, record the direction toward the end
+    {
+        int c = ey * w + ex;
+        int prev = -1;
+        p1x = ex;
+        p1y = ey;
+        while (true) {
+            const uint8_t pd = g.par[c] & 0x7f;
+            if (lane == 0) {
+                g.par[c] = (uint8_t)(pd | 0x80);
+                if (prev >= 0) {
+                    // direction from c to prev = opposite of prev's parent direction
+                    g.pdir[c] = (uint8_t)(((g.par[prev] & 0x7f) + 2) & 3);
+                } else {
+                    g.pdir[c] = kDirNone;
+                }
+            }
+            if (pd == kDirNone) break;  // reached the start
+            const int cx = c % w, cy = c / w;
+            const int nx = cx + ddx(pd), ny = cy + ddy(pd);
+            const int nxt = ny * w + nx;
+            if (nxt == s0) {
+                p1x = cx;
+                p1y = cy;
+            }
+            prev = c;
+            c = nxt;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    // set_key :252-259
+    kx = ky = -1;
+    for (int tries = 0; tries < kGenTries; tries++) {
+        const int x = rng.randint(0, w - 1);
+        const int y = rng.randint(0, h - 1);
+        const int c = y * w + x;
+        if (g.cell[c] == 1 || (x == ex && y == ey) || (x == sx && y == sy) || (g.par[c] & 0x80)) continue;
+        kx = x;
+        ky = y;
+        break;
+    }
+    return kx >= 0;
+}
+
+__device__ void generate_one(const mm_env_t& env, GenLds& g, int m) {
+    const int lane = threadIdx.x;
+    uint32_t* rs = env.rng + (size_t)m * MM_RNG_WORDS;
+    for (int k = lane; k < kMtN; k += 64) g.mt[k] = rs[k];
+    WaveRng rng;
+    rng.mt = g.mt;
+    rng.idx = (int)rs[kMtN];
+    rng.lane = lane;
+    __syncthreads();
+    int w, h, sx, sy, ex, ey, kx, ky, plen, p1x, p1y;
+    const bool ok = generate(env, g, rng, w, h, sx, sy, ex, ey, kx, ky, plen, p1x, p1y);
+    __syncthreads();
+    // final layout bytes: cell | dir-to-exit << 2
+    uint8_t* gl = env.layout + (size_t)m * env.layout_stride;
+    const int nc = w * h;
+    for (int c = lane; c < nc; c += 64) {
+        uint8_t b = g.cell[c];
+        if (b == 0) {
+            const uint8_t p = g.par[c];
+            const int d = (p & 0x80) ? g.pdir[c] : (p & 0x7f);
+            b = (uint8_t)(b | (d << 2));
+        }
+        gl[c] = b;
+    }
+    for (int k = lane; k < kMtN; k += 64) rs[k] = g.mt[k];
+    if (lane == 0) rs[kMtN] = (uint32_t)rng.idx;
+    __syncthreads();
+    if (lane == 0) {
+        mm_maze_t mz = env.mazes[m];
+        mz.t = 0;
+        mz.w = (int8_t)w; mz.h = (int8_t)h;
+        mz.ex = (int8_t)ex; mz.ey = (int8_t)ey;
+        mz.kx = (int8_t)kx; mz.ky = (int8_t)ky;
+        mz.sx = (int8_t)sx; mz.sy = (int8_t)sy;
+        mz.path_len = (int16_t)plen;
+        mz.spawn1 = p1x | (p1y << 8);  // second cell of the shortest path (agent 1's spawn)
+        if (!ok) mz.status |= MM_ST_GEN_FAIL;
+        env.mazes[m] = mz;
+    }
+}
+
+// Agent resets + the two reset observations (maze.py:64-71), one thread per
+// maze, reading the freshly generated layout from global memory.
+__device__ void reset_observe(const mm_env_t& env, int m, float* obs, uint8_t* masks) {
+    mm_maze_t mz = env.mazes[m];
+    View v;
+    v.L = env.layout + (size_t)m * env.layout_stride;
+    v.w = mz.w; v.h = mz.h; v.ex = mz.ex; v.ey = mz.ey; v.kx = mz.kx; v.ky = mz.ky;
+    v.t = 0; v.max_t = env.max_timestep;
+    Agent a0 = load_agent(env.agents[2 * m], 2);
+    Agent a1 = load_agent(env.agents[2 * m + 1], 3);
+    float* o = obs + (size_t)m * 2 * kObs;
+    uint8_t* mk = masks + (size_t)m * 2 * kMask;
+    // agent 0 resets and observes while agent 1 still holds its previous state (Q3)
+    reset_agent(a0, mz.sx, mz.sy);
+    observe(v, a0, a1, false, [&](int i, float x) { o[i] = x; }, mk);
+    reset_agent(a1, mz.spawn1 & 0xff, (mz.spawn1 >> 8) & 0xff);
+    observe(v, a1, a0, true, [&](int i, float x) { o[kObs + i] = x; }, mk + kMask);
+    env.agents[2 * m] = pack_agent(a0);
+    env.agents[2 * m + 1] = pack_agent(a1);
+}
+
+__global__ __launch_bounds__(256) void k_reset_obs(mm_env_t env, const uint8_t* __restrict__ mask, int use_list,
+                                                   float* obs, uint8_t* masks) {
+    const int count = use_list ? env.work[0] : env.n;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < count; k += gridDim.x * blockDim.x) {
+        const int m = use_list ? env.work[kListOff + k] : k;
+        if (!use_list && mask && !mask[m]) continue;
+        reset_observe(env, m, obs, masks);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __restrict__ mask, int use_list,
+                                              float* obs, uint8_t* masks) {
+    __shared__ GenLds g;
+    const int count = use_list ? env.work[0] : env.n;
+    for (int k = blockIdx.x; k < count; k += gridDim.x) {
+        const int m = use_list ? env.work[kListOff + k] : k;
+        if (!use_list && mask && !mask[m]) continue;
+        generate_one(env, g, m);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// step (one thread per maze)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kMPB) void k_step(mm_env_t env, const int8_t* __restrict__ act, float* __restrict__ obs,
+                                               uint8_t* __restrict__ masks, float* __restrict__ reward,
+                                               uint8_t* __restrict__ done, int list_done) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int stride = env.layout_stride;
+    const int lay_bytes = (kMPB * stride + 15) & ~15;
+    uint8_t* Ls = smem;
+    float* Os = reinterpret_cast<float*>(smem + lay_bytes);  // [kMPB][2][65]
+    uint8_t* Ms = reinterpret_cast<uint8_t*>(Os + kMPB * 2 * kObs);  // [kMPB][2][6]
+
+    const int m0 = blockIdx.x * kMPB;
+    const int nb = min(kMPB, env.n - m0);
+    copy_in(Ls, env.layout + (size_t)m0 * stride, nb * stride);
+    __syncthreads();
+
+    const int i = threadIdx.x;
+    const int m = m0 + i;
+    if (i < nb) {
+        mm_maze_t mz = env.mazes[m];
+        View v;
+        v.L = Ls + i * stride;
+        v.w = mz.w; v.h = mz.h; v.ex = mz.ex; v.ey = mz.ey; v.kx = mz.kx; v.ky = mz.ky;
+        v.max_t = env.max_timestep;
+        Agent a0 = load_agent(env.agents[2 * m], 2);
+        Agent a1 = load_agent(env.agents[2 * m + 1], 3);
+        const char4 ac = reinterpret_cast<const char4*>(act)[m];
+        uint32_t status = mz.status;
+        uint8_t* gl = env.layout + (size_t)m * stride;
+        // maze.py:75-90
+        mz.t += 1;
+        v.t = mz.t;
+        int first_key = agent_step(v, a0, ac.x, ac.y, gl, status);
+        int have_key = a0.f(MM_AF_HAS_KEY);
+        first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
+        have_key += a1.f(MM_AF_HAS_KEY);
+        // maze.py:99-113
+        float* o = Os + i * 2 * kObs;
+        uint8_t* mk = Ms + i * 2 * kMask;
+        const int am0 = observe(v, a0, a1, true, [&](int k, float x) { o[k] = x; }, mk);
+        bool exit_ready = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
+        const int am1 = observe(v, a1, a0, true, [&](int k, float x) { o[kObs + k] = x; }, mk + kMask);
+        exit_ready = exit_ready && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
+        if (exit_ready) {
+            const Agent* ags[2] = {&a0, &a1};
+            const int ams[2] = {am0, am1};
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                uint8_t* mq = mk + q * kMask;
+                if (!v.is_end(ags[q]->x, ags[q]->y)) {
+#pragma unroll
+                    for (int d = 0; d < 4; d++) mq[d] = (uint8_t)(d == ams[q]);
+                } else {
+                    mq[0] = mq[1] = mq[2] = mq[3] = 0;
+                    mq[4] = 1;
+                }
+            }
+        }
+        // reward / done :115-121
+        float r = first_key ? 0.5f * first_key : 0.f;
+        uint8_t dn = 0;
+        if (have_key && a0.x == a1.x && a0.y == a1.y && v.is_end(a0.x, a0.y)) {
+            r = 1.f;
+            dn = 1;
+        } else if (mz.t >= env.max_timestep) {
+            dn = 1;
+        }
+        reward[m] = r;
+        done[m] = dn;
+        mz.kx = (int8_t)v.kx;
+        mz.ky = (int8_t)v.ky;
+        mz.status = (uint16_t)status;
+        if (dn) {
+            mz.episodes += 1;
+            mz.last_len = mz.t;
+            mz.last_path = mz.path_len;
+            if (list_done) {
+                const int pos = atomicAdd(&env.work[0], 1);
+                env.work[kListOff + pos] = m;
+            }
+        }
+        env.mazes[m] = mz;
+        env.agents[2 * m] = pack_agent(a0);
+        env.agents[2 * m + 1] = pack_agent(a1);
+    }
+    __syncthreads();
+    copy_out(reinterpret_cast<uint8_t*>(obs + (size_t)m0 * 2 * kObs), reinterpret_cast<const uint8_t*>(Os),
+             nb * 2 * kObs * 4);
+    copy_out(masks + (size_t)m0 * 2 * kMask, Ms, nb * 2 * kMask);
+}
+
+inline size_t step_lds_bytes(int stride) {
+    return (size_t)((kMPB * stride + 15) & ~15) + (size_t)kMPB * 2 * kObs * 4 + (size_t)kMPB * 2 * kMask;
+}
+
+inline int check_env(const mm_env_t* env) {
+    if (!env || env->n <= 0 || !env->layout || !env->agents || !env->mazes || !env->rng || !env->work) return MM_E_ARG;
+    const int need = mm_layout_stride(env->size_w, env->size_h, env->rand_sizes, env->rand_lo, env->rand_hi);
+    if (need < 0 || env->size_w < 2 || env->size_h < 2) return MM_E_SIZE;
+    if (env->rand_sizes && (env->rand_lo < 2 || env->rand_hi < env->rand_lo)) return MM_E_SIZE;
+    if (env->layout_stride < need) return MM_E_SIZE;
+    if (env->difficulty < 1 || env->max_timestep < 1) return MM_E_ARG;
+    return 0;
+}
+
+}  // namespace mm
+
+using namespace mm;
+
+extern "C" int mm_version(void) { return 100; }
+
+extern "C" int mm_layout_stride(int size_w, int size_h, int rand_sizes, int rand_lo, int rand_hi) {
+    const int side = rand_sizes ? 2 * rand_hi - 1 : 2 * (size_w > size_h ? size_w : size_h) - 1;
+    if (side > MM_MAX_SIDE || side < 3) return MM_E_SIZE;
+    const int w = rand_sizes ? side : 2 * size_w - 1, h = rand_sizes ? side : 2 * size_h - 1;
+    return w * h;
+}
+
+extern "C" int mm_env_seed(const mm_env_t* env, const uint64_t* seeds, void* stream) {
+    int e = check_env(env);
+    if (e) return e;
+    if (!seeds) return MM_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_seed, dim3((env->n + 255) / 256), dim3(256), 0, s, *env, seeds);
+    return (int)hipGetLastError();
+}
+
+static int launch_reset(const mm_env_t* env, const uint8_t* mask, int use_list, float* obs, uint8_t* masks,
+                        hipStream_t s) {
+    int grid = use_list ? 2048 : (env->n < 16384 ? env->n : 16384);
+    hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), 0, s, *env, mask, use_list, obs, masks);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    const int ogrid = use_list ? 256 : (env->n + 255) / 256;
+    hipLaunchKernelGGL(k_reset_obs, dim3(ogrid), dim3(256), 0, s, *env, mask, use_list, obs, masks);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_env_reset(const mm_env_t* env, const uint8_t* reset_mask, float* obs, uint8_t* masks, void* stream) {
+    int e = check_env(env);
+    if (e) return e;
+    if (!obs || !masks) return MM_E_ARG;
+    return launch_reset(env, reset_mask, 0, obs, masks, (hipStream_t)stream);
+}
+
+extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward,
+                           uint8_t* done, int auto_reset, void* stream) {
+    int e = check_env(env);
+    if (e) return e;
+    if (!actions || !obs || !masks || !reward || !done) return MM_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (auto_reset) {
+        hipError_t me = hipMemsetAsync(env->work, 0, sizeof(int32_t), s);
+        if (me != hipSuccess) return (int)me;
+    }
+    const size_t lds = step_lds_bytes(env->layout_stride);
+    const int grid = (env->n + kMPB - 1) / kMPB;
+    hipLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB), lds, s, *env, actions, obs, masks, reward, done,
+                       auto_reset ? 1 : 0);
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return (int)le;
+    if (auto_reset) return launch_reset(env, nullptr, 1, obs, masks, s);
+    return 0;
+}

@@ -1,0 +1,160 @@
+// rl_kernels.hip -- PPO rollout-side kernels for MI355X (gfx950).
+//
+//   k_gae     PPO.get_GAEs (PPO.py:193-203) over a time-major [T, N] rollout,
+//             one lane per maze column: the reverse recursion is sequential in
+//             t by definition, the N columns are independent, and the [T, N]
+//             layout makes every step's loads/stores one coalesced row.
+//             fp32, no FMA contraction, the reference's operation order:
+//               delta_t = (r_t + f32(g*V_{t+1}) * (1-d_{t+1})) - V_t
+//               A_t     = delta_t + f32(f32(g*lam) * A_{t+1})   (0 if d_t)
+//             (the d_{t+1} mask drops V_{L-1} from delta_{L-2}: quirk Q7).
+//   k_sample  PPO.get_action (PPO.py:170-186) for every agent row: masked
+//             categorical move + Bernoulli mark, per-agent and joint log-prob,
+//             counter-based Philox4x32-10 draws.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "marlmaze.h"
+
+namespace mm {
+
+__global__ void k_gae(const float* __restrict__ rew, const float* __restrict__ val, const uint8_t* __restrict__ done,
+                      const float* __restrict__ last_val, int T, int N, float g, float gl, float* __restrict__ adv,
+                      float* __restrict__ rtg) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float a = 0.f;
+    // state carried from t+1: value and done flag
+    float v_next = last_val ? last_val[i] : 0.f;
+    bool have_next = last_val != nullptr;  // false: segment end == episode end
+    bool d_next = false;
+    for (int t = T - 1; t >= 0; t--) {
+        const size_t k = (size_t)t * N + i;
+        const float r = rew[k];
+        const float v = val[k];
+        // without a bootstrap value the segment end IS an episode end (done=1),
+        // so the reference's d_{t+1} mask also applies to delta_{T-2} (Q7)
+        const bool d = done[k] != 0 || (t == T - 1 && !last_val);
+        float delta;
+        if (d || !have_next) {
+            // the reference's `t+1 == len(ep)` branch: delta = r - V
+            delta = __fsub_rn(r, v);
+        } else {
+            float boot = __fmul_rn(g, v_next);
+            if (d_next) boot = __fmul_rn(boot, 0.f);
+            delta = __fsub_rn(__fadd_rn(r, boot), v);
+        }
+        const float scale = d ? 0.f : gl;
+        a = __fadd_rn(delta, __fmul_rn(scale, a));
+        adv[k] = a;
+        if (rtg) rtg[k] = __fadd_rn(a, v);  // b_rtgs = b_advs + b_vals (PPO.py:46)
+        v_next = v;
+        d_next = d;
+        have_next = true;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// One thread per maze: rows 2i (agent 0) and 2i+1 (agent 1).
+__global__ void k_sample(const float* __restrict__ ml, const float* __restrict__ kl, const uint8_t* __restrict__ masks,
+                         int M, uint64_t seed, uint64_t offset, int8_t* __restrict__ act, float* __restrict__ logp,
+                         float* __restrict__ joint) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nm = (M + 1) / 2;
+    if (i >= nm) return;
+    float jl = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; a++) {
+        const int row = 2 * i + a;
+        if (row >= M) break;
+        const uint4 rnd = philox(make_uint4((uint32_t)offset, (uint32_t)(offset >> 32), (uint32_t)row, 0u),
+                                 make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+        const uint8_t* mk = masks + (size_t)row * MM_MASK_DIM;
+        float l[5];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            l[j] = mk[j] ? ml[(size_t)row * 5 + j] : -INFINITY;  // masked_fill(~mask, -inf)
+            mx = fmaxf(mx, l[j]);
+        }
+        float p[5], sum = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            p[j] = mk[j] ? expf(l[j] - mx) : 0.f;
+            sum += p[j];
+        }
+        // inverse-CDF draw over the allowed moves
+        const float target = u01(rnd.x) * sum;
+        int move = -1, last = -1;
+        float c = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            if (!mk[j]) continue;
+            last = j;
+            c += p[j];
+            if (move < 0 && target < c) move = j;
+        }
+        if (move < 0) move = last;
+        float lp;
+        if (move < 0) {  // no legal move: the reference's Categorical is undefined (NaN)
+            move = 4;
+            lp = NAN;
+        } else {
+            lp = (l[move] - mx) - logf(sum);  // Categorical.log_prob = logit - logsumexp
+        }
+        // mark ~ Bernoulli(sigmoid(mark_logit)) if allowed else 0 (PPO.py:179-181)
+        int mark = 0;
+        float pm = 0.f;
+        if (mk[5]) {
+            pm = 1.f / (1.f + expf(-kl[row]));
+            mark = u01(rnd.y) < pm ? 1 : 0;
+        }
+        lp += logf(mark ? pm : 1.f - pm);
+        act[2 * row] = (int8_t)move;
+        act[2 * row + 1] = (int8_t)mark;
+        if (logp) logp[row] = lp;
+        jl += lp;
+    }
+    if (joint) joint[i] = jl;
+}
+
+}  // namespace mm
+
+using namespace mm;
+
+extern "C" int mm_gae(const float* reward, const float* value, const uint8_t* done, const float* last_value, int T,
+                      int N, float gamma, float gamma_lambda, float* adv, float* rtg, void* stream) {
+    if (!reward || !value || !done || !adv || T < 0 || N < 0) return MM_E_ARG;
+    if (T == 0 || N == 0) return 0;
+    hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, reward, value, done,
+                       last_value, T, N, gamma, gamma_lambda, adv, rtg);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M,
+                         uint64_t seed, uint64_t offset, int8_t* actions, float* logp, float* joint_logp,
+                         void* stream) {
+    if (!move_logits || !mark_logits || !masks || !actions || M < 0) return MM_E_ARG;
+    if (M == 0) return 0;
+    const int nm = (M + 1) / 2;
+    hipLaunchKernelGGL(k_sample, dim3((nm + 255) / 256), dim3(256), 0, (hipStream_t)stream, move_logits, mark_logits,
+                       masks, M, seed, offset, actions, logp, joint_logp);
+    return (int)hipGetLastError();
+}

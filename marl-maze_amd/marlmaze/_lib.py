@@ -1,0 +1,98 @@
+"""ctypes binding of libmarlmaze.so (the C ABI declared in include/marlmaze.h).
+
+The library is the product: there is no CPU fallback.  Importing this module
+on a machine without the built library raises immediately, and every call
+checks the returned status code.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first: the .so binds to it)
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "libmarlmaze.so")
+
+OBS_DIM = 65
+MASK_DIM = 6
+RNG_WORDS = 625
+MAX_SIDE = 41
+MAZES_PER_BLOCK = 64
+
+ST_GEN_FAIL = 1
+ST_BAD_MOVE = 2
+
+AF_KNOWS_END = 1
+AF_SEES_END = 2
+AF_OTHER_KNOWS = 4
+AF_HAS_KEY = 8
+AF_SEES_KEY = 16
+AF_TEAM_KEY = 32
+AF_HAS_MARK = 64
+
+# exported symbols (tests check every one of them is present)
+EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
+           "mm_env_step", "mm_gae", "mm_sample")
+
+
+class EnvDesc(ctypes.Structure):
+    """mirror of mm_env_t"""
+    _fields_ = [
+        ("n", ctypes.c_int32), ("size_w", ctypes.c_int32), ("size_h", ctypes.c_int32),
+        ("max_timestep", ctypes.c_int32), ("difficulty", ctypes.c_int32),
+        ("rand_start", ctypes.c_int32), ("rand_sizes", ctypes.c_int32),
+        ("rand_lo", ctypes.c_int32), ("rand_hi", ctypes.c_int32),
+        ("layout_stride", ctypes.c_int32),
+        ("layout", ctypes.c_void_p), ("agents", ctypes.c_void_p), ("mazes", ctypes.c_void_p),
+        ("rng", ctypes.c_void_p), ("work", ctypes.c_void_p),
+    ]
+
+
+_LIB = None
+
+
+class MMError(RuntimeError):
+    pass
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise MMError(
+                f"libmarlmaze.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+                "There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        P, i32, u64, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_float
+        L.mm_version.restype = i32
+        L.mm_layout_stride.argtypes = [i32] * 5
+        L.mm_layout_stride.restype = i32
+        L.mm_env_seed.argtypes = [ctypes.POINTER(EnvDesc), P, P]
+        L.mm_env_seed.restype = i32
+        L.mm_env_reset.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P]
+        L.mm_env_reset.restype = i32
+        L.mm_env_step.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P, P, i32, P]
+        L.mm_env_step.restype = i32
+        L.mm_gae.argtypes = [P, P, P, P, i32, i32, f32, f32, P, P, P]
+        L.mm_gae.restype = i32
+        L.mm_sample.argtypes = [P, P, P, i32, u64, u64, P, P, P, P]
+        L.mm_sample.restype = i32
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what):
+    if rc != 0:
+        raise MMError(f"{what} failed with status {rc}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

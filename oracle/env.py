@@ -94,15 +94,13 @@ class OracleEnv:
     def reset_all(self):
         obs = np.zeros((self.n, 2, OBS_DIM), np.float32)
         masks = np.zeros((self.n, 2, MASK_DIM), np.uint8)
-        if lib().oenv_reset_all(self._h, _p(obs), _p(masks)):
-            raise RuntimeError("oracle: maze generation failed (key placement)")
+        lib().oenv_reset_all(self._h, _p(obs), _p(masks))  # failures: maze(i)["error"] & 1
         return obs, masks.astype(bool)
 
     def reset(self, i):
         obs = np.zeros((2, OBS_DIM), np.float32)
         masks = np.zeros((2, MASK_DIM), np.uint8)
-        if lib().oenv_reset(self._h, i, _p(obs), _p(masks)):
-            raise RuntimeError("oracle: maze generation failed (key placement)")
+        lib().oenv_reset(self._h, i, _p(obs), _p(masks))  # failures: maze(i)["error"] & 1
         return obs, masks.astype(bool)
 
     def step(self, i, action):
@@ -120,16 +118,14 @@ class OracleEnv:
         masks = np.zeros((self.n, 2, MASK_DIM), np.uint8)
         r = np.zeros(self.n, np.float32)
         d = np.zeros(self.n, np.uint8)
-        if lib().oenv_step_all(self._h, _p(act), _p(obs), _p(masks), _p(r),
-                               _p(d), int(auto_reset)):
-            raise RuntimeError("oracle: maze generation failed (key placement)")
+        lib().oenv_step_all(self._h, _p(act), _p(obs), _p(masks), _p(r), _p(d), int(auto_reset))
         return obs, masks.astype(bool), r, d.astype(bool)
 
     # -- introspection
     def maze(self, i):
         info = np.zeros(12, np.int32)
-        layout = np.zeros(39 * 39, np.uint8)
-        path = np.zeros((39 * 39, 2), np.int16)
+        layout = np.zeros(41 * 41, np.uint8)
+        path = np.zeros((41 * 41, 2), np.int16)
         lib().oenv_get_maze(self._h, i, _p(info), _p(layout), _p(path))
         w, h = int(info[0]), int(info[1])
         return dict(w=w, h=h, start=(int(info[2]), int(info[3])),
@@ -139,6 +135,9 @@ class OracleEnv:
                     error=int(info[11]),
                     layout=layout[:w * h].reshape(h, w).copy(),
                     path=path[:int(info[9])].copy())
+
+    def errors(self):
+        return np.array([self.maze(i)["error"] for i in range(self.n)], np.int32)
 
     def agent(self, i, a):
         out = np.zeros(N_ASTATE, np.int32)

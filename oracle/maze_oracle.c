@@ -35,7 +35,11 @@
 #define OBS_DIM 65
 #define MASK_DIM 6
 #define ROUTE_CAP 8192
-#define KEY_TRIES_MAX 1000000 /* maze.py:254 loops forever on some tiny mazes */
+/* maze.py:244-250 / 254-259 loop forever when no cell qualifies (e.g. a tiny
+ * maze whose every path cell lies on the shortest path).  Both this oracle and
+ * the HIP kernels give up after GEN_TRIES draws with the same protocol: set_end
+ * failure -> end = start, path = [start], no key; set_key failure -> no key. */
+#define GEN_TRIES 65536
 
 /* ------------------------------------------------------------------------ */
 /* CPython MT19937                                                           */
@@ -143,11 +147,11 @@ typedef struct {
 
 typedef struct {
     int w, h;
-    uint8_t layout[39 * 39 + 64];
+    uint8_t layout[41 * 41 + 64];
     int sx, sy, ex, ey;
     int key_valid, kx, ky;
     int path_len;
-    int16_t path[39 * 39 + 64][2];
+    int16_t path[41 * 41 + 64][2];
     int t;
     int error;
     PyRng rng;
@@ -178,20 +182,21 @@ static void set_start(const OEnv* e, OMaze* m) { /* maze.py:229-237 */
     }
 }
 
-static void set_end(OMaze* m) { /* maze.py:239-250 */
+static int set_end(OMaze* m) { /* maze.py:239-250 */
     int coin = rng_randint(&m->rng, 0, 1);
     int x = coin == 0 ? 0 : m->w - 1;
-    for (;;) {
+    for (long tries = 0; tries < GEN_TRIES; tries++) {
         int y = rng_randint(&m->rng, 0, m->h - 1);
         if (x == m->sx && y == m->sy) continue;
-        if (CELL(m, x, y) == 0) { m->ex = x; m->ey = y; return; }
+        if (CELL(m, x, y) == 0) { m->ex = x; m->ey = y; return 0; }
     }
+    return -1;
 }
 
 /* Unique start->end path in the spanning tree (maze.py:261-273 DFS result). */
 static int tree_path(const OMaze* m, int16_t (*out)[2]) {
-    static int16_t par[39 * 39 + 64];
-    static int16_t q[39 * 39 + 64];
+    static int16_t par[41 * 41 + 64];
+    static int16_t q[41 * 41 + 64];
     int n = m->w * m->h;
     for (int i = 0; i < n; i++) par[i] = -2;
     int head = 0, tail = 0, s = m->sy * m->w + m->sx, goal = m->ey * m->w + m->ex;
@@ -228,7 +233,7 @@ static int build_maze(const OEnv* e, OMaze* m) { /* maze.py:170-218 */
     memset(m->layout, 1, (size_t)(m->w * m->h));
     set_start(e, m);
     /* recursive backtracker: maze.py:180-201 */
-    static int16_t stk[39 * 39][2];
+    static int16_t stk[41 * 41][2];
     int sp = 0;
     stk[sp][0] = (int16_t)m->sx;
     stk[sp][1] = (int16_t)m->sy;
@@ -259,7 +264,17 @@ static int build_maze(const OEnv* e, OMaze* m) { /* maze.py:170-218 */
     /* difficulty x (set_end + path); last end among the longest wins (maze.py:204-217) */
     int best_len = 0, bex = 0, bey = 0;
     for (int r = 0; r < e->difficulty; r++) {
-        set_end(m);
+        if (set_end(m)) { /* give up: end = start, path = [start], no key */
+            m->ex = m->sx;
+            m->ey = m->sy;
+            m->path_len = 1;
+            m->path[0][0] = (int16_t)m->sx;
+            m->path[0][1] = (int16_t)m->sy;
+            m->path[1][0] = (int16_t)m->sx;
+            m->path[1][1] = (int16_t)m->sy;
+            m->key_valid = 0;
+            return -1;
+        }
         int len = tree_path(m, m->path);
         if (len > best_len) best_len = len;
         if (len == best_len) { bex = m->ex; bey = m->ey; }
@@ -268,8 +283,9 @@ static int build_maze(const OEnv* e, OMaze* m) { /* maze.py:170-218 */
     m->ey = bey;
     m->path_len = tree_path(m, m->path);
     /* set_key: maze.py:252-259 */
+    m->key_valid = 0;
     for (long tries = 0;; tries++) {
-        if (tries > KEY_TRIES_MAX) return -1;
+        if (tries >= GEN_TRIES) return -1;
         int x = rng_randint(&m->rng, 0, m->w - 1);
         int y = rng_randint(&m->rng, 0, m->h - 1);
         if (CELL(m, x, y) == 1 || (x == m->ex && y == m->ey) || (x == m->sx && y == m->sy)) continue;
@@ -519,14 +535,15 @@ static void observe(OEnv* e, OMaze* m, int self_i, const Positions* pos, float* 
 /* Maze.reset: maze.py:55-72 */
 static int maze_reset(OEnv* e, OMaze* m, float* obs, uint8_t* masks) {
     m->t = 0;
-    if (build_maze(e, m)) { m->error |= 1; return -1; }
+    int rc = 0;
+    if (build_maze(e, m)) { m->error |= 1; rc = -1; }
     Positions pos = {0, {0, 0}};
     for (int i = 0; i < 2; i++) {
         agent_reset(&m->ag[i], m->path[i][0], m->path[i][1]);
         pos.idx[pos.n++] = i;
         observe(e, m, i, &pos, obs + i * OBS_DIM, masks + i * MASK_DIM);
     }
-    return 0;
+    return rc;
 }
 
 /* single_agent_step: maze.py:124-163; returns got_key */

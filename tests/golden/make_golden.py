@@ -282,7 +282,7 @@ def fresh_ppo(**kw):
 
 def sd_to_np(prefix, sd, out):
     for k, v in sd.items():
-        out[prefix + k] = v.detach().cpu().numpy()
+        out[prefix + k] = v.detach().cpu().numpy().copy()
 
 
 def capture_gae():
@@ -391,9 +391,14 @@ def capture_ckpt_logits():
     with torch.no_grad():
         mv, mr = brain.actor(torch.as_tensor(obs).reshape(-1, 65))
         v = brain.critic(torch.as_tensor(obs))
+    w = {}
+    sd_to_np("actor/", sd["actor"], w)
+    sd_to_np("critic/", sd["critic"], w)
+    w["adam_step"] = np.float32(sd["actor_optim"]["state"][0]["step"])
+    w["adam_lr"] = np.float64(sd["actor_optim"]["param_groups"][0]["lr"])
     np.savez_compressed(os.path.join(OUT, "ckpt_logits.npz"), obs=obs,
                         move_logits=mv.numpy(), mark_logits=mr.numpy(),
-                        values=v.numpy())
+                        values=v.numpy(), **w)
     print("ckpt_logits: move logit mean", mv.mean(0).numpy())
 
 

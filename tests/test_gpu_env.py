@@ -1,0 +1,180 @@
+"""GPU parity of the HIP environment (libmarlmaze.so via VecMaze) -- bit-exact.
+
+Checks the HIP path against (a) the reference's own golden vectors and (b) the
+C oracle on large batches of independent mazes driven by random legal play,
+at the BASELINE configurations' maze sizes (10x10 and 20x20, 65,536 mazes).
+"""
+import numpy as np
+import pytest
+import torch
+
+from marlmaze.vecmaze import VecMaze
+from oracle.env import OracleEnv
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg_kwargs(c):
+    return dict(default_size=(int(c[0]), int(c[1])), difficulty=int(c[3]), rand_start=bool(c[2]),
+                rand_sizes=bool(c[4]), rand_range=(int(c[5]), int(c[6])))
+
+
+def test_generation_matches_reference(golden):
+    g = golden("maze_gen")
+    for ci, c in enumerate(g["case_cfg"]):
+        ks = np.nonzero((g["case"] == ci) & (g["reset"] == 0))[0]
+        seeds = [int(g["seed"][k]) for k in ks]
+        env = VecMaze(len(ks), max_timestep=1200, seeds=seeds, **_cfg_kwargs(c))
+        for r in range(3):
+            obs, masks = env.reset()
+            obs, masks = obs.cpu().numpy(), masks.cpu().numpy().astype(bool)
+            info = env.maze_info()
+            lays = env.layouts()
+            assert not info["status"].any()
+            for j, k in enumerate(ks):
+                kk = k + r
+                assert (info["w"][j], info["h"][j]) == (g["w"][kk], g["h"][kk])
+                assert (info["sx"][j], info["sy"][j]) == tuple(g["start"][kk])
+                assert (info["ex"][j], info["ey"][j]) == tuple(g["end"][kk])
+                assert (info["kx"][j], info["ky"][j]) == tuple(g["key"][kk])
+                assert info["path_len"][j] == g["path_len"][kk]
+                assert np.array_equal(np.asarray(env.shortest_path(j)), g["path"][kk][:g["path_len"][kk]])
+                assert np.array_equal(lays[j], g["layout"][kk][:info["h"][j], :info["w"][j]])
+                assert np.array_equal(env.get_rng(j), g["mt"][kk])
+                assert np.array_equal(obs[j], g["obs"][kk]), (ci, j, r)
+                assert np.array_equal(masks[j], g["masks"][kk]), (ci, j, r)
+
+
+@pytest.mark.parametrize("auto_reset", [False, True])
+def test_trajectories_match_reference(golden, auto_reset):
+    t = golden("env_traj")
+    for name in t["names"]:
+        cfg = t[name + "/cfg"]
+        env = VecMaze(1, default_size=(int(cfg[0]), int(cfg[1])), max_timestep=int(cfg[2]),
+                      difficulty=int(cfg[3]), rand_start=bool(cfg[4]), rand_sizes=bool(cfg[5]),
+                      rand_range=(int(cfg[6]), int(cfg[7])), seeds=[int(cfg[8])])
+        obs, masks = env.reset()
+        assert np.array_equal(obs.cpu().numpy()[0], t[name + "/obs0"])
+        assert np.array_equal(masks.cpu().numpy()[0].astype(bool), t[name + "/masks0"])
+        A = torch.as_tensor(t[name + "/actions"]).cuda()
+        for s in range(len(A)):
+            obs, masks, r, d = env.step(A[s:s + 1], auto_reset=auto_reset)
+            if not auto_reset:
+                st = env.agent_state(0)
+                assert np.array_equal(st, t[name + "/astate"][s]), (name, s, st, t[name + "/astate"][s])
+                if bool(d[0]):
+                    env.reset(d)
+            assert float(r[0]) == t[name + "/reward"][s] and bool(d[0]) == t[name + "/done"][s], (name, s)
+            assert np.array_equal(obs.cpu().numpy()[0], t[name + "/obs"][s]), (name, s)
+            assert np.array_equal(masks.cpu().numpy()[0].astype(bool), t[name + "/masks"][s]), (name, s)
+        assert not env.status().any()
+
+
+def test_policy_trajectory_matches_reference(golden):
+    """Trajectory whose actions the reference PPO.pth policy sampled."""
+    t = golden("env_ppo")
+    env = VecMaze(1, default_size=(6, 6), max_timestep=150, seeds=[21])
+    obs, masks = env.reset()
+    assert np.array_equal(obs.cpu().numpy()[0], t["obs0"])
+    A = torch.as_tensor(t["actions"]).cuda()
+    for s in range(len(A)):
+        obs, masks, r, d = env.step(A[s:s + 1], auto_reset=True)
+        assert np.array_equal(obs.cpu().numpy()[0], t["obs"][s]), s
+        assert np.array_equal(masks.cpu().numpy()[0].astype(bool), t["masks"][s]), s
+        assert float(r[0]) == t["reward"][s] and bool(d[0]) == t["done"][s]
+
+
+def random_legal(rng, masks):
+    """masks [n,2,6] bool -> actions [n,2,2] int8: uniform legal move, mark ~ B(0.5) if allowed."""
+    mv = masks[..., :5]
+    u = rng.random(mv.shape) * mv
+    move = np.argmax(u, axis=-1)
+    move = np.where(mv.any(-1), move, 4)
+    mark = (rng.random(masks.shape[:2]) < 0.5) & masks[..., 5]
+    return np.stack([move, mark], -1).astype(np.int8)
+
+
+CONFIGS = {
+    "10x10": dict(default_size=(10, 10), max_timestep=150),
+    "20x20": dict(default_size=(20, 20), max_timestep=120),
+    "4x4_t30": dict(default_size=(4, 4), max_timestep=30),
+    "main_cfg": dict(default_size=(4, 4), max_timestep=60, rand_sizes=True, rand_range=(12, 13),
+                     rand_start=True),
+    "d3_rs": dict(default_size=(7, 5), max_timestep=40, rand_start=True, difficulty=3),
+}
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_random_play_matches_oracle(name):
+    cfg = CONFIGS[name]
+    n, steps = 2048, 260
+    seeds = np.arange(n, dtype=np.uint64) * np.uint64(7919) + np.uint64(3)
+    env = VecMaze(n, seeds=seeds, **cfg)
+    ora = OracleEnv(n, seeds=seeds, **cfg)
+    go, gm = env.reset()
+    oo, om = ora.reset_all()
+    assert np.array_equal(go.cpu().numpy(), oo) and np.array_equal(gm.cpu().numpy().astype(bool), om)
+    rng = np.random.default_rng(1)
+    masks = om
+    n_done = 0
+    for s in range(steps):
+        act = random_legal(rng, masks)
+        go, gm, gr, gd = env.step(torch.as_tensor(act).cuda(), auto_reset=True)
+        oo, om, orw, od = ora.step_all(act, auto_reset=True)
+        gd = gd.cpu().numpy().astype(bool)
+        assert np.array_equal(gd, od), s
+        assert np.array_equal(gr.cpu().numpy(), orw), s
+        assert np.array_equal(go.cpu().numpy(), oo), s
+        gmn = gm.cpu().numpy().astype(bool)
+        assert np.array_equal(gmn, om), s
+        masks = om
+        n_done += int(od.sum())
+    assert n_done > 0
+    # generation give-ups (the reference would hang) must coincide exactly
+    assert np.array_equal(env.status() & 1, ora.errors() & 1)
+    assert not (env.status() & 2).any()
+    for i in range(0, n, 97):
+        assert np.array_equal(env.agent_state(i), np.stack([ora.agent(i, a) for a in range(2)])), i
+        lay = ora.maze(i)["layout"]
+        assert np.array_equal(env.layouts()[i], lay), i
+
+
+def test_65536_mazes_10x10_match_oracle():
+    """configs[2] scale: 65,536 parallel 10x10 mazes, bit-exact vs the oracle."""
+    n, steps = 65536, 24
+    cfg = dict(default_size=(10, 10), max_timestep=1200)
+    env = VecMaze(n, **cfg)
+    ora = OracleEnv(n, **cfg)
+    go, gm = env.reset()
+    oo, om = ora.reset_all()
+    assert np.array_equal(go.cpu().numpy(), oo)
+    rng = np.random.default_rng(2)
+    masks = om
+    for s in range(steps):
+        act = random_legal(rng, masks)
+        go, gm, gr, gd = env.step(torch.as_tensor(act).cuda(), auto_reset=True)
+        oo, om, orw, od = ora.step_all(act, auto_reset=True)
+        assert np.array_equal(go.cpu().numpy(), oo), s
+        assert np.array_equal(gm.cpu().numpy().astype(bool), om), s
+        assert np.array_equal(gr.cpu().numpy(), orw) and np.array_equal(gd.cpu().numpy().astype(bool), od)
+        masks = om
+
+
+def test_reset_mask_and_independence():
+    """Resetting a subset leaves the other mazes untouched; per-maze streams are
+    independent of the batch they live in (seed i behaves the same alone)."""
+    cfg = dict(default_size=(6, 6), max_timestep=50)
+    seeds = np.array([5, 17, 99, 1234], np.uint64)
+    big = VecMaze(4, seeds=seeds, **cfg)
+    big.reset()
+    lay0 = [l.copy() for l in big.layouts()]
+    mask = torch.tensor([0, 1, 0, 1], dtype=torch.uint8, device="cuda")
+    big.reset(mask)
+    lay1 = big.layouts()
+    assert np.array_equal(lay0[0], lay1[0]) and np.array_equal(lay0[2], lay1[2])
+    for j in (1, 3):
+        single = VecMaze(1, seeds=[int(seeds[j])], **cfg)
+        single.reset()
+        single.reset()
+        assert np.array_equal(single.layouts()[0], lay1[j])
+        assert np.array_equal(single.get_rng(0), big.get_rng(j))

@@ -1,0 +1,118 @@
+"""GPU parity of the GAE scan and the action sampler (libmarlmaze.so)."""
+import numpy as np
+import pytest
+import torch
+
+from marlmaze import ops
+from oracle import ppo as oppo
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gae_matches_reference_vectors(golden):
+    g = golden("gae")
+    for i in range(int(g["n"])):
+        r = torch.as_tensor(g[f"L{i}/rew"].astype(np.float32)).cuda()[:, None]
+        v = torch.as_tensor(g[f"L{i}/val"]).cuda()[:, None]
+        d = torch.as_tensor(g[f"L{i}/done"]).cuda()[:, None]
+        adv, rtg = ops.gae(r, v, d)
+        assert np.array_equal(adv[:, 0].cpu().numpy(), g[f"L{i}/adv"].astype(np.float32)), i
+        assert np.array_equal(rtg[:, 0].cpu().numpy(), (g[f"L{i}/adv"].astype(np.float32) + g[f"L{i}/val"]))
+
+
+def _split_episodes(r, v, d):
+    """oracle: per-column episodes (segment end = episode end), reference GAE each."""
+    T, N = r.shape
+    out = np.zeros((T, N), np.float32)
+    for n in range(N):
+        s = 0
+        for t in range(T):
+            if d[t, n] or t == T - 1:
+                dd = d[s:t + 1, n].copy()
+                dd[-1] = True
+                out[s:t + 1, n] = oppo.gae_fp32(list(r[s:t + 1, n].astype(np.float64)), v[s:t + 1, n], dd)
+                s = t + 1
+    return out
+
+
+@pytest.mark.parametrize("T,N", [(1, 7), (16, 257), (64, 1000)])
+def test_gae_time_major_matches_oracle(T, N):
+    rng = np.random.default_rng(T * 1000 + N)
+    r = rng.choice(np.float32([0, 0, 0, 0.5, 1]), size=(T, N)).astype(np.float32)
+    v = rng.normal(0, 1, (T, N)).astype(np.float32)
+    d = rng.random((T, N)) < 0.1
+    adv, rtg = ops.gae(torch.as_tensor(r).cuda(), torch.as_tensor(v).cuda(), torch.as_tensor(d).cuda())
+    assert np.array_equal(adv.cpu().numpy(), _split_episodes(r, v, d))
+    assert np.array_equal(rtg.cpu().numpy(), adv.cpu().numpy() + v)
+
+
+def test_gae_bootstrap_and_scale():
+    T, N = 32, 65536  # configs: 65,536 mazes, T=32
+    rng = np.random.default_rng(0)
+    r = rng.choice(np.float32([0, 0.5, 1]), size=(T, N)).astype(np.float32)
+    v = rng.normal(0, 1, (T, N)).astype(np.float32)
+    d = rng.random((T, N)) < 0.02
+    lv = rng.normal(0, 1, N).astype(np.float32)
+    adv, _ = ops.gae(*(torch.as_tensor(x).cuda() for x in (r, v, d)), last_value=torch.as_tensor(lv).cuda())
+    # numpy fp32 emulation of the bootstrapped recursion
+    f = np.float32
+    g, gl = f(0.99), f(0.99 * 0.95)
+    a = np.zeros(N, np.float32)
+    vn, dn = lv.copy(), np.zeros(N, bool)
+    ref = np.zeros((T, N), np.float32)
+    for t in range(T - 1, -1, -1):
+        boot = (g * vn).astype(np.float32)
+        boot = np.where(dn, (boot * f(0)).astype(np.float32), boot)
+        delta = np.where(d[t], (r[t] - v[t]).astype(np.float32), ((r[t] + boot).astype(np.float32) - v[t]))
+        a = (delta + np.where(d[t], f(0), gl) * a).astype(np.float32)
+        ref[t] = a
+        vn, dn = v[t], d[t]
+    assert np.array_equal(adv.cpu().numpy(), ref)
+
+
+def _random_masks(rng, M):
+    m = rng.random((M, 6)) < 0.6
+    none = ~m[:, :5].any(1)
+    m[none, rng.integers(0, 5, none.sum())] = True
+    return m
+
+
+def test_sampler_logp_and_legality():
+    M = 2 * 50000
+    rng = np.random.default_rng(3)
+    ml = rng.normal(0, 2, (M, 5)).astype(np.float32)
+    kl = rng.normal(0, 2, (M, 1)).astype(np.float32)
+    mk = _random_masks(rng, M)
+    a, lp, jl = ops.sample(*(torch.as_tensor(x).cuda() for x in (ml, kl, mk.astype(np.uint8))), seed=7, offset=0)
+    a = a.cpu().numpy().astype(np.int64)
+    assert mk[np.arange(M), a[:, 0]].all()  # legal moves only
+    assert (a[~mk[:, 5], 1] == 0).all()  # no mark where not allowed
+    # log-prob formula of PPO.get_log_probs / get_action on the CPU (torch)
+    o = torch.as_tensor
+    ref = oppo.log_probs(lambda x: (o(ml), o(kl)), 0, o(np.zeros((M, 1, 65), np.float32)),
+                         o(a[:, None, :].astype(np.float32)), o(mk[:, None, :]))
+    np.testing.assert_allclose(lp.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=1e-6)
+    j = lp.cpu().numpy().reshape(-1, 2)
+    assert np.array_equal(jl.cpu().numpy(), (j[:, 0] + j[:, 1]).astype(np.float32))
+    # determinism (counter-based): same (seed, offset) -> same draw; new offset -> new draw
+    a2, _, _ = ops.sample(*(torch.as_tensor(x).cuda() for x in (ml, kl, mk.astype(np.uint8))), seed=7, offset=0)
+    a3, _, _ = ops.sample(*(torch.as_tensor(x).cuda() for x in (ml, kl, mk.astype(np.uint8))), seed=7, offset=1)
+    assert np.array_equal(a2.cpu().numpy(), a)
+    assert not np.array_equal(a3.cpu().numpy(), a)
+
+
+def test_sampler_distribution():
+    M = 400000
+    logits = np.float32([1.0, -0.5, 0.3, 2.0, -1.0])
+    ml = np.tile(logits, (M, 1))
+    kl = np.full((M, 1), 0.7, np.float32)
+    mk = np.ones((M, 6), bool)
+    mk[:, 2] = False
+    a, _, _ = ops.sample(*(torch.as_tensor(x).cuda() for x in (ml, kl, mk.astype(np.uint8))), seed=11, offset=5)
+    a = a.cpu().numpy()
+    p = np.exp(logits - logits.max()) * mk[0, :5]
+    p /= p.sum()
+    freq = np.bincount(a[:, 0], minlength=5) / M
+    assert np.abs(freq - p).max() < 4 * np.sqrt(p.max() / M) + 1e-4
+    pm = 1 / (1 + np.exp(-0.7))
+    assert abs(a[:, 1].mean() - pm) < 4 * np.sqrt(pm * (1 - pm) / M)
