@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Headline benchmark: PPO training throughput over parallel 2-agent mazes.
+
+BASELINE.json metric: "env-steps/sec (2-agent 10x10 maze) + PPO updates/sec at
+1/2/4/8 MI355X".  One bench *step* = one full PPO iteration on every GPU:
+rollout of ``horizon`` env-steps in each of ``mazes`` mazes (critic + actor
+forward, sampler kernel, env-step kernel, auto-reset), the GAE scan, and the
+update of PPO.py:46-85 (5 epochs x 5 minibatches, clipped surrogate + value
+MSE, one flat-gradient all-reduce per minibatch under DP, Adam).
+
+value = env-steps/s of the WHOLE job (all ranks, rollout + update time).
+Default workload: 65,536 10x10 mazes per GPU (BASELINE configs[2] scale, the
+north-star's 1M env-steps/s target) running configs[1]'s rollout+update loop.
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]
+        python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "marl-maze_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from marlmaze.PPO import PPO  # noqa: E402
+from marlmaze.dist import DP  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def cpu_baseline(seconds=12.0, size=10, max_t=1200):
+    """The oracle's single-maze PPO.train() port on the host cores (bounded sample)."""
+    from oracle.env import OracleEnv
+    from oracle.ppo import CpuPPOPort
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    env = OracleEnv(1, default_size=(size, size), max_timestep=max_t, seeds=[0])
+    port = CpuPPOPort(env, batch_size=15000, lr=1.4e-4)
+    # rollout: as many steps as fit in ~2/3 of the budget (PPO.py:108-141 per step)
+    t0 = time.time()
+    steps = 0
+    chunk = 200
+    batches = []
+    while time.time() - t0 < seconds * 0.66:
+        n, batch = port.get_batch(max_steps=chunk)
+        steps += n
+        batches.append(batch)
+    t_roll = time.time() - t0
+    merged = [torch.cat([b[k] for b in batches]) for k in range(6)]
+    port.batch_size = len(merged[0]) - len(merged[0]) % 5
+    t1 = time.time()
+    hist = port.update(merged)  # 5 x 5 minibatch updates of batch_size//5 (PPO.py:51-85)
+    t_upd = time.time() - t1
+    return dict(value=steps / (t_roll + t_upd), unit="env-steps/s", cores=threads, kind="port",
+                sample=f"oracle CpuPPOPort (C env + torch CPU fp32, 1 maze {size}x{size}, max_t {max_t}): "
+                       f"{steps} rollout steps in {t_roll:.1f}s + {len(hist)} minibatch updates of "
+                       f"{port.batch_size // 5} in {t_upd:.1f}s",
+                rollout_env_steps_per_s=steps / t_roll, ppo_updates_per_s=len(hist) / t_upd)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--mazes", type=int, default=65536, help="mazes per GPU")
+    ap.add_argument("--size", type=int, default=10, help="default_size (cells); layout is 2*size-1")
+    ap.add_argument("--horizon", type=int, default=16, help="env-steps per maze per iteration")
+    ap.add_argument("--max-t", type=int, default=1200, help="max_timestep (main.py:20)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    a = ap.parse_args()
+
+    dp = DP.from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    world = dp.world
+    if world != a.gpus and dp.rank == 0:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    n, T = a.mazes, a.horizon
+    samples_local = n * T
+    batch_global = 5 * ((samples_local * world) // 5)
+    agent = PPO(2, epochs=1, batch_size=batch_global, lr=1.4e-4, n_envs=n, horizon=T, load=False, verbose=False,
+                save=False, dp=dp, sample_seed=12345,
+                env_config=dict(default_size=(a.size, a.size), max_timestep=a.max_t, seed_base=0))
+
+    def iteration():
+        b = agent.rollout()
+        B = T * n
+        agent.update(b["obs"][:T].reshape(B, 2, 65), b["act"].reshape(B, 2, 2), b["logp"].reshape(B),
+                     b["masks"][:T].reshape(B, 2, 6), b["adv"].reshape(B), b["val"].reshape(B))
+        agent._carry_over()
+
+    for _ in range(a.warmup):
+        iteration()
+    torch.cuda.synchronize()
+    dp.barrier()
+
+    agent.step_events = []
+    upd_ev = []
+    t0 = time.time()
+    for _ in range(a.steps):
+        b = agent.rollout()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        B = T * n
+        agent.update(b["obs"][:T].reshape(B, 2, 65), b["act"].reshape(B, 2, 2), b["logp"].reshape(B),
+                     b["masks"][:T].reshape(B, 2, 6), b["adv"].reshape(B), b["val"].reshape(B))
+        e1.record()
+        upd_ev.append((e0, e1))
+        agent._carry_over()
+    torch.cuda.synchronize()
+    dp.barrier()
+    elapsed = time.time() - t0
+    if dp.active:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    step_ms = [s.elapsed_time(e) for s, e in agent.step_events]
+    upd_ms = [s.elapsed_time(e) for s, e in upd_ev]
+    env_step_ms = float(np.mean(step_ms))
+    H = 2 * a.size - 1
+    alg_bytes = H * H + 703  # layout + marks + agents r/w + maze r/w + actions + obs + masks + reward + done
+    achieved = n * alg_bytes / (env_step_ms * 1e-3) / 1e9
+    n_updates = len(agent.history) or None
+    minibatches_per_iter = agent.updates_per_batch * len(range(0, batch_global // world, (batch_global // world) // 5))
+    total_steps = world * n * T * a.steps
+
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", f"pmc_env_step_{n}x{a.size}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    line = {
+        "metric": "env-steps/sec (2-agent 10x10 maze) + PPO updates/sec",
+        "value": total_steps / elapsed,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: procedurally generated mazes (CPython-MT seeds 0..N-1 per GPU), random-init "
+                "actor/critic (torch.manual_seed(3234)), actions sampled by the policy",
+        "config": {
+            "workload": f"PPO rollout+GAE+update over {n} parallel {a.size}x{a.size} 2-agent mazes per GPU "
+                        f"(configs[1] loop at configs[2] scale)",
+            "mazes_per_gpu": n, "maze": f"{a.size}x{a.size} (layout {H}x{H})", "max_timestep": a.max_t,
+            "horizon": T, "global_batch": batch_global, "minibatch": batch_global // 5,
+            "minibatch_steps_per_iter": minibatches_per_iter, "parallelism": f"dp{world}",
+        },
+        "ppo_updates_per_sec": minibatches_per_iter * a.steps / elapsed,
+        "update_ms_per_iter": float(np.mean(upd_ms)),
+        "rollout_env_steps_per_sec": total_steps / (elapsed - sum(upd_ms) * 1e-3),
+        "roofline": {
+            "kernel": "k_step (mm_env_step)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+            "alg_bytes_per_env_step": alg_bytes, "launch_us": env_step_ms * 1e3, "launches": len(step_ms),
+        },
+    }
+    del n_updates
+    if dp.rank == 0:
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dp.active:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -124,10 +124,18 @@ int mm_env_reset(const mm_env_t* env, const uint8_t* reset_mask, float* obs, uin
 
 /* Maze.step(actions) for every maze.  actions [n,2,2] int8 = (move, mark) per
  * agent.  Outputs obs [n,2,65] f32, masks [n,2,6] u8, reward [n] f32,
- * done [n] u8.  With auto_reset != 0 the finished mazes are regenerated and
- * their obs/mask rows replaced by the reset observation (PPO.py:127-130). */
+ * done [n] u8, and (if ep_stats != NULL) ep_stats [n,2] int32 = (episode
+ * length, shortest_path_len) where done, (0,0) elsewhere (PPO.py:129,131).
+ * auto_reset = 1: the finished mazes are regenerated and their obs/mask rows
+ * replaced by the reset observation (PPO.py:127-130); = 2: the finished
+ * mazes are only queued, for a later mm_env_reset_done (lets a caller time
+ * or overlap the step kernel alone); = 0: nothing is reset or queued. */
 int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward, uint8_t* done,
-                int auto_reset, void* stream);
+                int32_t* ep_stats, int auto_reset, void* stream);
+
+/* Maze.reset() for the mazes queued by the previous mm_env_step(auto_reset=2)
+ * (writes their obs/mask rows; clears the queue). */
+int mm_env_reset_done(const mm_env_t* env, float* obs, uint8_t* masks, void* stream);
 
 /* Time-major GAE over [T, N] (PPO.py:193-203, episodes concatenated in time,
  * done[t] = the transition at t ended its episode).  last_value [N] (may be

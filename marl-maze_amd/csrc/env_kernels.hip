@@ -306,18 +306,31 @@ __device__ void reset_observe(const mm_env_t& env, int m, float* obs, uint8_t* m
 
 __global__ __launch_bounds__(256) void k_reset_obs(mm_env_t env, const uint8_t* __restrict__ mask, int use_list,
                                                    float* obs, uint8_t* masks) {
-    const int count = use_list ? env.work[0] : env.n;
+    const int count = use_list ? min(env.work[0], env.n) : env.n;
     for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < count; k += gridDim.x * blockDim.x) {
         const int m = use_list ? env.work[kListOff + k] : k;
         if (!use_list && mask && !mask[m]) continue;
         reset_observe(env, m, obs, masks);
+    }
+    if (use_list) {
+        // Done list consumed: the LAST block to finish clears the counter for
+        // the next step (every block read work[0] above, before taking its
+        // ticket).  Kernel boundaries order this against the next k_step.
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int ticket = atomicAdd(&env.work[1], 1);
+            if (ticket == (int)gridDim.x - 1) {
+                env.work[0] = 0;
+                env.work[1] = 0;
+            }
+        }
     }
 }
 
 __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __restrict__ mask, int use_list,
                                               float* obs, uint8_t* masks) {
     __shared__ GenLds g;
-    const int count = use_list ? env.work[0] : env.n;
+    const int count = use_list ? min(env.work[0], env.n) : env.n;
     for (int k = blockIdx.x; k < count; k += gridDim.x) {
         const int m = use_list ? env.work[kListOff + k] : k;
         if (!use_list && mask && !mask[m]) continue;
@@ -331,7 +344,8 @@ __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __res
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kMPB) void k_step(mm_env_t env, const int8_t* __restrict__ act, float* __restrict__ obs,
                                                uint8_t* __restrict__ masks, float* __restrict__ reward,
-                                               uint8_t* __restrict__ done, int list_done) {
+                                               uint8_t* __restrict__ done, int32_t* __restrict__ ep_stats,
+                                               int list_done) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int stride = env.layout_stride;
     const int lay_bytes = (kMPB * stride + 15) & ~15;
@@ -397,6 +411,8 @@ __global__ __launch_bounds__(kMPB) void k_step(mm_env_t env, const int8_t* __res
         }
         reward[m] = r;
         done[m] = dn;
+        if (ep_stats)  // (episode length, shortest_path_len) of an episode that ended here (PPO.py:129,131)
+            reinterpret_cast<int2*>(ep_stats)[m] = dn ? make_int2(mz.t, mz.path_len) : make_int2(0, 0);
         mz.kx = (int8_t)v.kx;
         mz.ky = (int8_t)v.ky;
         mz.status = (uint16_t)status;
@@ -406,7 +422,7 @@ __global__ __launch_bounds__(kMPB) void k_step(mm_env_t env, const int8_t* __res
             mz.last_path = mz.path_len;
             if (list_done) {
                 const int pos = atomicAdd(&env.work[0], 1);
-                env.work[kListOff + pos] = m;
+                if (pos < env.n) env.work[kListOff + pos] = m;  // (queue not drained by the caller: ignore)
             }
         }
         env.mazes[m] = mz;
@@ -474,21 +490,25 @@ extern "C" int mm_env_reset(const mm_env_t* env, const uint8_t* reset_mask, floa
 }
 
 extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward,
-                           uint8_t* done, int auto_reset, void* stream) {
+                           uint8_t* done, int32_t* ep_stats, int auto_reset, void* stream) {
     int e = check_env(env);
     if (e) return e;
     if (!actions || !obs || !masks || !reward || !done) return MM_E_ARG;
+    if (auto_reset < 0 || auto_reset > 2) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
-    if (auto_reset) {
-        hipError_t me = hipMemsetAsync(env->work, 0, sizeof(int32_t), s);
-        if (me != hipSuccess) return (int)me;
-    }
     const size_t lds = step_lds_bytes(env->layout_stride);
     const int grid = (env->n + kMPB - 1) / kMPB;
-    hipLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB), lds, s, *env, actions, obs, masks, reward, done,
+    hipLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB), lds, s, *env, actions, obs, masks, reward, done, ep_stats,
                        auto_reset ? 1 : 0);
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
-    if (auto_reset) return launch_reset(env, nullptr, 1, obs, masks, s);
+    if (auto_reset == 1) return launch_reset(env, nullptr, 1, obs, masks, s);
     return 0;
+}
+
+extern "C" int mm_env_reset_done(const mm_env_t* env, float* obs, uint8_t* masks, void* stream) {
+    int e = check_env(env);
+    if (e) return e;
+    if (!obs || !masks) return MM_E_ARG;
+    return launch_reset(env, nullptr, 1, obs, masks, (hipStream_t)stream);
 }

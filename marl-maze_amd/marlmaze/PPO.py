@@ -1,0 +1,356 @@
+"""PPO over N parallel mazes on one or more MI355X -- the reference's PPO API.
+
+Mirrors ``PPO`` of the reference (PPO.py:11-238): same constructor arguments,
+same methods (train, get_batch, get_action, get_log_probs, get_state_values,
+get_GAEs, get_rtgs, decay_lr, save/load_parameters), same checkpoint dict
+(``actor``, ``critic``, ``actor_optim``, ``critic_optim``) so ``PPO.pth`` files
+move both ways.  What changes is where the work runs:
+
+* rollout: ``n_envs`` mazes step together in HBM (VecMaze, HIP kernels); per
+  step one critic call on all [N, 130] observations, one actor call on all
+  [2N, 65] agent rows, one sampler kernel (masked Categorical + Bernoulli,
+  PPO.py:170-186) and one env-step kernel.  No host synchronisation inside
+  the rollout.
+* GAE: one HIP scan over the time-major [T, N] buffers (PPO.get_GAEs,
+  PPO.py:193-203, bit-exact fp32).
+* update: the clipped-surrogate + value-MSE minibatch loop of PPO.py:46-85,
+  both losses in one backward, one flat gradient all-reduce under data
+  parallelism (marlmaze.dist), clip_grad_norm_ per network, Adam.
+
+Rollout semantics: the reference collects whole episodes from ONE maze until
+more than ``batch_size`` steps are stored (PPO.py:108-141).  Here every maze
+advances ``horizon`` steps per batch and episodes continue across batches; a
+segment that ends mid-episode is bootstrapped with V(s_T) (``bootstrap=True``)
+or treated as an episode end exactly like the reference's last step
+(``bootstrap=False``).  The minibatch loop keeps the reference's quirk Q8
+(it spans ``batch_size``, not the number of samples collected).
+"""
+import math
+import os
+import random
+
+import numpy as np
+import torch
+
+from . import ops
+from .dist import DP
+from .networks import Actor, Critic
+from .vecmaze import VecMaze
+
+MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
+
+
+class PPO:
+    def __init__(self, agent_amount, epochs=500, batch_size=15000, lr=0.0002, discount_rate=0.99, lam=0.95,
+                 updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
+                 seed=3234, sample_seed=None, device=None, model_path=MODEL_PATH, load=True, parity_mode=True,
+                 bootstrap=True, dp=None, verbose=True, save=True):
+        self.maze = None  # wired by Maze.__init__ (maze.py:39-42), as in the reference
+        self.dp = dp if dp is not None else DP.single()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        # networks are built on the CPU right after the seed, like PPO.py:7,16-17
+        g = torch.random.get_rng_state()
+        torch.manual_seed(seed)
+        self.actor = Actor([264, 264, 264], parity_mode=parity_mode).to(self.device)
+        self.critic = Critic(agent_amount, hidden_sizes=[64, 64]).to(self.device)
+        torch.random.set_rng_state(g)
+        self.dp.broadcast_params([self.actor, self.critic])
+        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=lr)
+        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=lr)
+
+        self.agent_amount = agent_amount
+        self.epochs = epochs
+        self.batch_size = batch_size
+        self.lr = lr
+        self.discount_rate = discount_rate
+        self.lam = lam
+        self.updates_per_batch = updates_per_batch
+        self.mbatch_size = self.batch_size // 5
+        self.clip = clip
+        self.max_grad = max_grad
+
+        self.n_envs = int(n_envs)
+        self.horizon = int(horizon) if horizon else max(1, math.ceil(batch_size / (self.n_envs * self.dp.world)))
+        self.env_config = env_config
+        self.bootstrap = bootstrap
+        self.sample_seed = (sample_seed if sample_seed is not None else random.getrandbits(63)) + 7919 * self.dp.rank
+        self._sample_offset = 0
+        self.model_path = model_path
+        self.verbose = verbose and self.dp.rank == 0
+        self.save = save
+        self.venv = None
+        self._bufs = None
+        self.history = []
+        self.step_events = None  # list -> rollout records (start, end) events around each env step
+        if load:
+            self.load_parameters()
+
+    # ------------------------------------------------------------------
+    # environment + buffers
+    # ------------------------------------------------------------------
+    def _env_kwargs(self):
+        if self.env_config is not None:
+            return dict(self.env_config)
+        m = self.maze
+        if m is None:
+            return dict(default_size=(10, 10), max_timestep=1200)
+        return dict(default_size=tuple(m.default_size), max_timestep=m.max_timestep, difficulty=m.difficulty,
+                    rand_start=m.rand_start, rand_sizes=m.rand_sizes, rand_range=tuple(m.rand_range))
+
+    def _ensure_env(self):
+        if self.venv is not None:
+            return
+        n = self.n_envs
+        base = int(self.env_config.get("seed_base", 0)) if self.env_config else random.getrandbits(32)
+        kw = {k: v for k, v in self._env_kwargs().items() if k != "seed_base"}
+        seeds = np.arange(n, dtype=np.uint64) + np.uint64(base) + np.uint64(self.dp.rank * n)
+        self.venv = VecMaze(n, seeds=seeds, device=self.device, **kw)
+        T, d = self.horizon, self.device
+        self._bufs = dict(
+            obs=torch.zeros((T + 1, n, 2, 65), dtype=torch.float32, device=d),
+            masks=torch.zeros((T + 1, n, 2, 6), dtype=torch.uint8, device=d),
+            act=torch.zeros((T, n, 2, 2), dtype=torch.int8, device=d),
+            logp=torch.zeros((T, n), dtype=torch.float32, device=d),
+            rowlogp=torch.zeros((T, 2 * n), dtype=torch.float32, device=d),
+            val=torch.zeros((T, n), dtype=torch.float32, device=d),
+            last_val=torch.zeros((n,), dtype=torch.float32, device=d),
+            rew=torch.zeros((T, n), dtype=torch.float32, device=d),
+            done=torch.zeros((T, n), dtype=torch.uint8, device=d),
+            stats=torch.zeros((T, n, 2), dtype=torch.int32, device=d),
+            adv=torch.zeros((T, n), dtype=torch.float32, device=d),
+            rtg=torch.zeros((T, n), dtype=torch.float32, device=d),
+        )
+        self.venv.reset(obs=self._bufs["obs"][0], masks=self._bufs["masks"][0])
+
+    # ------------------------------------------------------------------
+    # rollout (PPO.get_batch, PPO.py:89-152)
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def rollout(self):
+        """Advance every maze ``horizon`` steps; fills the [T, N] buffers."""
+        self._ensure_env()
+        b, n, T = self._bufs, self.n_envs, self.horizon
+        for t in range(T):
+            obs_t = b["obs"][t]
+            b["val"][t] = self.critic(obs_t).view(n)
+            ml, kl = self.actor(obs_t.view(2 * n, 65))
+            ops.sample(ml, kl, b["masks"][t].view(2 * n, 6), self.sample_seed, self._sample_offset,
+                       actions=b["act"][t].view(2 * n, 2), logp=b["rowlogp"][t], joint_logp=b["logp"][t])
+            self._sample_offset += 1
+            ev = self.step_events
+            if ev is None:
+                self.venv.step(b["act"][t], auto_reset=True, obs=b["obs"][t + 1], masks=b["masks"][t + 1],
+                               reward=b["rew"][t], done=b["done"][t], ep_stats=b["stats"][t])
+            else:  # instrumented: time the env-step kernel alone (HIP events on this stream)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self.venv.step(b["act"][t], auto_reset=2, obs=b["obs"][t + 1], masks=b["masks"][t + 1],
+                               reward=b["rew"][t], done=b["done"][t], ep_stats=b["stats"][t])
+                e1.record()
+                self.venv.reset_done(obs=b["obs"][t + 1], masks=b["masks"][t + 1])
+                ev.append((e0, e1))
+        last = None
+        if self.bootstrap:
+            b["last_val"].copy_(self.critic(b["obs"][T]).view(n))
+            last = b["last_val"]
+        ops.gae(b["rew"], b["val"], b["done"], last_value=last, gamma=self.discount_rate, lam=self.lam,
+                adv=b["adv"], rtg=b["rtg"])
+        return b
+
+    def _carry_over(self):
+        """The next batch starts from the last observation (episodes continue)."""
+        b = self._bufs
+        b["obs"][0].copy_(b["obs"][self.horizon])
+        b["masks"][0].copy_(b["masks"][self.horizon])
+
+    def get_batch(self):
+        """Reference 8-tuple (PPO.py:151-152), samples flattened time-major."""
+        b = self.rollout()
+        T, n = self.horizon, self.n_envs
+        B = T * n
+        out = (b["obs"][:T].reshape(B, 2, 65).clone(), b["act"].reshape(B, 2, 2).float(),
+               b["logp"].reshape(B).clone(), None, None, b["masks"][:T].reshape(B, 2, 6).bool(),
+               b["adv"].reshape(B).clone(), b["val"].reshape(B).clone())
+        st = b["stats"].reshape(B, 2)
+        fin = st[:, 0] > 0
+        ep_lens = st[fin, 0].tolist()
+        shortest = st[fin, 1].tolist()
+        self._carry_over()
+        return out[:3] + (shortest, ep_lens) + out[5:]
+
+    # ------------------------------------------------------------------
+    # update (PPO.py:46-85)
+    # ------------------------------------------------------------------
+    def policy_logp(self, obs, act, masks):
+        """Sum over agents of get_log_probs (PPO.py:66-68), one actor call on [2M, 65]."""
+        M = obs.shape[0]
+        ml, kl = self.actor(obs.reshape(2 * M, 65))
+        mk = masks.reshape(2 * M, 6).bool()
+        a = act.reshape(2 * M, 2)
+        ml = ml.masked_fill(~mk[:, 0:5], float("-inf"))
+        lp = torch.log_softmax(ml, dim=-1).gather(1, a[:, 0:1].long()).squeeze(1)
+        kl = kl.squeeze(1).masked_fill(~mk[:, 5], float("-inf"))
+        p = torch.sigmoid(kl)
+        p = torch.where(a[:, 1] != 0, p, 1 - p)
+        lp = (lp + torch.log(p)).view(M, 2)
+        return lp[:, 0] + lp[:, 1]
+
+    def minibatch_step(self, obs, act, old_logp, adv, rtg, masks):
+        V = self.critic(obs).view(-1)
+        cur = self.policy_logp(obs, act, masks)
+        ratio = torch.exp(cur - old_logp)
+        s1 = ratio * adv
+        s2 = torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv
+        actor_loss = -torch.mean(torch.min(s1, s2))
+        critic_loss = torch.nn.functional.mse_loss(V, rtg)
+        self.actor_optim.zero_grad(set_to_none=False)
+        self.critic_optim.zero_grad(set_to_none=False)
+        (actor_loss + critic_loss).backward()  # disjoint parameters: same grads as two backwards
+        params = list(self.actor.parameters()) + list(self.critic.parameters())
+        self.dp.allreduce_grads(params)
+        gna = torch.nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad)
+        gnc = torch.nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad)
+        self.actor_optim.step()
+        self.critic_optim.step()
+        return actor_loss.detach(), critic_loss.detach(), gna.detach(), gnc.detach()
+
+    def update(self, b_obs, b_act, b_logp, b_masks, b_advs, b_vals, index_list=None, generator=None):
+        """Update body of PPO.train; returns per-minibatch (aloss, closs, gnorm_a, gnorm_c) [K, 4]."""
+        b_rtgs = b_advs + b_vals
+        mean, std = self.dp.global_mean_std(b_advs)
+        b_advs = (b_advs - mean) / (std + 1e-10)
+        B = b_obs.shape[0]
+        if index_list is None:
+            index_list = torch.randperm(B, device=b_obs.device, generator=generator)
+        else:
+            index_list = torch.as_tensor(index_list, device=b_obs.device, dtype=torch.long)
+        local_bs = min(self.batch_size // self.dp.world, B) if self.dp.active else self.batch_size
+        mb = local_bs // 5 if self.dp.active else self.mbatch_size
+        hist = []
+        for _ in range(self.updates_per_batch):
+            self.decay_lr()
+            for start in range(0, local_bs, mb):
+                idx = index_list[start:start + mb]
+                hist.append(torch.stack(self.minibatch_step(b_obs[idx], b_act[idx], b_logp[idx], b_advs[idx],
+                                                            b_rtgs[idx], b_masks[idx])))
+        hist = torch.stack(hist)
+        if self.dp.active:  # local losses -> global-minibatch losses (equal shards); norms are already global
+            self.dp.allreduce_sum(hist)
+            hist /= self.dp.world
+        return hist
+
+    def train(self):
+        for epoch in range(self.epochs):
+            b_obs, b_act, b_lp, b_sp, ep_lens, b_masks, b_advs, b_vals = self.get_batch()
+            hist = self.update(b_obs, b_act, b_lp, b_masks, b_advs, b_vals)
+            stats = dict(epoch=epoch, episodes=len(ep_lens), mean_len=float(np.mean(ep_lens)) if ep_lens else 0.0,
+                         mean_shortest=float(np.mean(b_sp)) if b_sp else 0.0,
+                         actor_loss=float(hist[-1, 0]), critic_loss=float(hist[-1, 1]))
+            self.history.append(stats)
+            if self.verbose:  # PPO.py:37-44, condensed
+                print(f"-------------------- Epoch #{epoch} --------------------")
+                print(f"Mazes solved in current epoch: {stats['episodes']}")
+                print(f"Average Exit Time: {stats['mean_len']}")
+                print(f"Average Length of Shortest Path: {stats['mean_shortest']}", flush=True)
+            if self.save and self.dp.rank == 0:
+                self.save_parameters()
+
+    # ------------------------------------------------------------------
+    # single-sample API of the reference
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def get_action(self, obs, action_mask):
+        """PPO.get_action (PPO.py:170-186): ([move, mark], log_prob (1,1))."""
+        ml, kl = self.actor(obs)
+        mk = torch.as_tensor(np.asarray(action_mask, dtype=np.uint8), device=self.device).view(1, 6)
+        a, lp, _ = ops.sample(ml, kl.reshape(-1), mk, self.sample_seed, self._sample_offset)
+        self._sample_offset += 1
+        a = a.cpu().tolist()[0]
+        return [a[0], a[1]], lp.view(1, 1)
+
+    def get_log_probs(self, i, batch_obs, batch_actions, batch_masks):
+        """PPO.get_log_probs (PPO.py:154-168)."""
+        moves, marks = batch_actions[:, i, 0], batch_actions[:, i, 1]
+        ml, kl = self.actor(batch_obs[:, i, :])
+        ml = ml.masked_fill(~batch_masks[:, i, 0:5], float("-inf"))
+        lp = torch.log_softmax(ml, dim=-1).gather(1, moves.long().view(-1, 1)).squeeze(1)
+        kl = kl.squeeze(1).masked_fill(~batch_masks[:, i, 5], float("-inf"))
+        p = torch.sigmoid(kl)
+        p = torch.where(marks.to(torch.bool), p, 1 - p)
+        return lp + torch.log(p)
+
+    def get_state_values(self, batch_obs):
+        return self.critic(batch_obs).squeeze()
+
+    def get_GAEs(self, ep_rew, ep_values, ep_dones):
+        """PPO.get_GAEs (PPO.py:193-203) on the GPU scan; returns a float64 array like the reference."""
+        L = len(ep_rew)
+        r = torch.as_tensor(np.asarray(ep_rew, np.float32), device=self.device).view(L, 1)
+        v = torch.as_tensor(np.asarray([float(x) for x in ep_values], np.float32), device=self.device).view(L, 1)
+        d = torch.as_tensor(np.asarray(ep_dones, np.uint8), device=self.device).view(L, 1)
+        d[-1] = 1  # the reference's t+1 == L branch ends the episode
+        adv, _ = ops.gae(r, v, d, gamma=self.discount_rate, lam=self.lam)
+        return adv.view(L).cpu().numpy().astype(np.float64)
+
+    def get_rtgs(self, batch_rew):
+        """PPO.get_rtgs (PPO.py:205-214): logging helper, 0.995 discount."""
+        rtgs = []
+        for episode_rew in reversed(batch_rew):
+            acc = 0
+            for rew in reversed(episode_rew):
+                acc = rew + 0.995 * acc
+                rtgs.append(acc)
+        rtgs.reverse()
+        return rtgs
+
+    def decay_lr(self):
+        for opt in (self.actor_optim, self.critic_optim):  # PPO.py:216-220
+            for group in opt.param_groups:
+                group["lr"] *= 0.997
+
+    def save_parameters(self):
+        torch.save({"actor": self.actor.state_dict(), "critic": self.critic.state_dict(),
+                    "actor_optim": self.actor_optim.state_dict(),
+                    "critic_optim": self.critic_optim.state_dict()}, self.model_path)
+
+    def load_parameters(self):
+        if os.path.exists(self.model_path):
+            sd = torch.load(self.model_path, weights_only=True, map_location=self.device)
+            self.actor.load_state_dict(sd["actor"])
+            self.critic.load_state_dict(sd["critic"])
+            self.actor_optim.load_state_dict(sd["actor_optim"])
+            self.critic_optim.load_state_dict(sd["critic_optim"])
+            if self.verbose:
+                print("successfuly loaded existing parameters")
+            return True
+        return False
+
+
+def smoke_iteration():
+    """One tiny rollout + update on cuda:0, checked against the CPU oracle's update."""
+    import oracle.ppo as oppo
+
+    agent = PPO(2, epochs=1, batch_size=1280, lr=1.4e-4, n_envs=256, horizon=5, load=False, verbose=False,
+                save=False, env_config=dict(default_size=(10, 10), max_timestep=60, seed_base=0), sample_seed=1)
+    b_obs, b_act, b_lp, _, _, b_masks, b_adv, b_val = agent.get_batch()
+    assert torch.isfinite(b_lp).all() and torch.isfinite(b_adv).all()
+    # teacher-forced comparison of one minibatch update with the oracle (CPU fp32)
+    actor, critic = oppo.OActor(), oppo.OCritic()
+    actor.load_state_dict({k: v.cpu() for k, v in agent.actor.state_dict().items()})
+    critic.load_state_dict({k: v.cpu() for k, v in agent.critic.state_dict().items()})
+    aopt = torch.optim.Adam(actor.parameters(), lr=1.4e-4)
+    copt = torch.optim.Adam(critic.parameters(), lr=1.4e-4)
+    idx = torch.arange(256)
+    adv = torch.randn(256, generator=torch.Generator().manual_seed(0))
+    rtg = torch.randn(256, generator=torch.Generator().manual_seed(1))
+    ref = oppo.minibatch_step(actor, critic, aopt, copt, b_obs[idx].cpu(), b_act[idx].cpu(), b_lp[idx].cpu(),
+                              adv, rtg, b_masks[idx].cpu())
+    got = agent.minibatch_step(b_obs[idx], b_act[idx], b_lp[idx], adv.cuda(), rtg.cuda(), b_masks[idx])
+    got = [float(x) for x in got]
+    for g, r in zip(got, ref):  # losses and gradient norms: 1e-5 relative
+        assert abs(g - r) <= 1e-5 * abs(r) + 1e-7, (got, ref)
+    # Adam's first step is lr * g/|g|: parameters move by <= lr; agree far below that
+    for k, p in actor.state_dict().items():
+        np.testing.assert_allclose(agent.actor.state_dict()[k].cpu().numpy(), p.numpy(), rtol=0, atol=2.1e-4)

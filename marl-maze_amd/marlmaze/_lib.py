@@ -31,7 +31,7 @@ AF_HAS_MARK = 64
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
-           "mm_env_step", "mm_gae", "mm_sample")
+           "mm_env_step", "mm_env_reset_done", "mm_gae", "mm_sample")
 
 
 class EnvDesc(ctypes.Structure):
@@ -71,8 +71,10 @@ def lib():
         L.mm_env_seed.restype = i32
         L.mm_env_reset.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P]
         L.mm_env_reset.restype = i32
-        L.mm_env_step.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P, P, i32, P]
+        L.mm_env_step.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P, P, P, i32, P]
         L.mm_env_step.restype = i32
+        L.mm_env_reset_done.argtypes = [ctypes.POINTER(EnvDesc), P, P, P]
+        L.mm_env_reset_done.restype = i32
         L.mm_gae.argtypes = [P, P, P, P, i32, i32, f32, f32, P, P, P]
         L.mm_gae.restype = i32
         L.mm_sample.argtypes = [P, P, P, i32, u64, u64, P, P, P, P]

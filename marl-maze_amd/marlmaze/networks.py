@@ -1,0 +1,137 @@
+"""Actor / Critic of the reference (networks.py:13-106), laid out for MI355X.
+
+Parameters keep the reference's module tree and ``state_dict`` names (so the
+shipped ``PPO.pth`` loads unchanged) and are created in the reference's order,
+so ``torch.manual_seed(s)`` gives the same initial weights.  ``forward`` does
+not replay the reference's 23 tiny Linear calls: the 23 feature embeddings are
+packed into ONE [460, k] GEMM, Q/K/V into ONE [20, 40] GEMM over all 23
+tokens, the two heads into ONE [264, 6] GEMM -- all fp32 GEMMs on the f32 MFMA
+path (hipBLASLt) -- with the same arithmetic per output element.
+
+Quirk Q1 (networks.py:59-63): the reference never advances the slice index,
+so every embedding reads ``x[:, 0:d_i]`` and the actor sees only obs[0:4].
+``parity_mode=True`` (default) keeps that; ``parity_mode=False`` gives each
+feature its own slice (what the code evidently intended).
+"""
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+FEATURE_DIMS = [4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 2, 2, 1, 4, 1, 1, 1, 1, 1, 1, 2]  # networks.py:8
+FEATURE_AMOUNT = len(FEATURE_DIMS)
+OBS_SPACE = int(np.sum(FEATURE_DIMS))  # 65
+EMBEDDING_DIM = 20
+KQ_DIM = 10
+_SQRT_KQ = float(np.sqrt(KQ_DIM))  # networks.py:79 divides by np.sqrt(10)
+
+
+class Projection(nn.Module):
+    """networks.py:51-65 -- 23 Linear(d_i -> 20); forward packs them into one GEMM."""
+
+    def __init__(self, parity_mode=True):
+        super().__init__()
+        self.layers = nn.ModuleList([nn.Linear(d, EMBEDDING_DIM) for d in FEATURE_DIMS])
+        self.parity_mode = parity_mode
+        starts = np.zeros(FEATURE_AMOUNT, np.int64) if parity_mode else np.cumsum([0] + FEATURE_DIMS[:-1])
+        self.register_buffer("_starts", torch.as_tensor(starts), persistent=False)
+        self.in_width = 4 if parity_mode else OBS_SPACE
+
+    def packed(self):
+        """W [460, in_width] (zero outside each feature's slice), b [460]."""
+        rows = []
+        for lin, d, s in zip(self.layers, FEATURE_DIMS, self._starts.tolist()):
+            w = lin.weight
+            left = s
+            right = self.in_width - s - d
+            rows.append(F.pad(w, (left, right)))
+        return torch.cat(rows, 0), torch.cat([lin.bias for lin in self.layers], 0)
+
+    def forward(self, x, packed=None):
+        W, b = packed if packed is not None else self.packed()
+        return F.linear(x[:, :self.in_width], W, b)  # [B, 460] = 23 embeddings of 20
+
+
+class m_Attention(nn.Module):
+    """networks.py:67-82 -- one self-attention layer over the 23 feature tokens."""
+
+    def __init__(self, kq_dim=KQ_DIM):
+        super().__init__()
+        self.kq_dim = kq_dim
+        self.keys = nn.Linear(EMBEDDING_DIM, kq_dim, bias=False)
+        self.querys = nn.Linear(EMBEDDING_DIM, kq_dim, bias=False)
+        self.values = nn.Linear(EMBEDDING_DIM, EMBEDDING_DIM, bias=False)
+
+    def forward(self, h):
+        B = h.shape[0]
+        t = h.view(B, FEATURE_AMOUNT, EMBEDDING_DIM)
+        wqkv = torch.cat([self.querys.weight, self.keys.weight, self.values.weight], 0)  # [40, 20]
+        qkv = F.linear(t, wqkv)  # [B, 23, 40]
+        q, k, v = qkv.split([self.kq_dim, self.kq_dim, EMBEDDING_DIM], dim=-1)
+        logits = torch.bmm(q, k.transpose(1, 2)) / _SQRT_KQ  # [B, 23, 23]
+        w = torch.softmax(logits, dim=-1)
+        ctx = torch.bmm(w, v)
+        return (t + ctx).reshape(B, FEATURE_AMOUNT * EMBEDDING_DIM)
+
+
+class Actor(nn.Module):
+    """networks.py:13-48.  forward(x) -> [move_logits [B,5], mark_logit [B,1]]."""
+
+    def __init__(self, hidden_sizes=(164, 164, 164, 164, 164), activation=nn.ReLU, parity_mode=True):
+        super().__init__()
+        hidden_sizes = list(hidden_sizes)
+        self.projection = Projection(parity_mode)
+        self.attention = m_Attention()
+        self.layers = nn.ModuleList()
+        self.activation = activation
+        self.layers.append(nn.Linear(FEATURE_AMOUNT * EMBEDDING_DIM, hidden_sizes[0]))
+        for a, b in zip(hidden_sizes[:-1], hidden_sizes[1:]):
+            self.layers.append(nn.Linear(a, b))
+        self.move_head = nn.Linear(hidden_sizes[-1], 5)
+        self.mark_head = nn.Linear(hidden_sizes[-1], 1)
+        self.initialize_weights()
+
+    def initialize_weights(self):  # networks.py:43-48
+        for layer in self.layers:
+            nn.init.orthogonal_(layer.weight)
+        with torch.no_grad():
+            self.move_head.weight *= 0.01
+            self.mark_head.weight *= 0.01
+
+    def forward(self, x):
+        x = torch.as_tensor(x, dtype=torch.float32, device=self.move_head.weight.device).reshape(-1, OBS_SPACE)
+        h = self.attention(self.projection(x))
+        act = F.relu if self.activation is nn.ReLU else self.activation()
+        for lin in self.layers:
+            h = act(lin(h))
+        heads = F.linear(h, torch.cat([self.move_head.weight, self.mark_head.weight], 0),
+                         torch.cat([self.move_head.bias, self.mark_head.bias], 0))
+        return [heads[:, :5], heads[:, 5:6]]
+
+
+class Critic(nn.Module):
+    """networks.py:84-106.  forward(x [.., agents, 65]) -> V [B, 1]."""
+
+    def __init__(self, agent_amount, hidden_sizes=(128, 128), activation=nn.ReLU):
+        super().__init__()
+        hidden_sizes = list(hidden_sizes)
+        self.layers = nn.ModuleList()
+        self.activation = activation
+        self.agent_amount = agent_amount
+        self.layers.append(nn.Linear(agent_amount * OBS_SPACE, hidden_sizes[0]))
+        for a, b in zip(hidden_sizes[:-1], hidden_sizes[1:]):
+            self.layers.append(nn.Linear(a, b))
+        self.layers.append(nn.Linear(hidden_sizes[-1], 1))
+        self.initialize_weights()
+
+    def initialize_weights(self):  # networks.py:104-106
+        for layer in self.layers:
+            nn.init.orthogonal_(layer.weight)
+
+    def forward(self, x):
+        x = torch.as_tensor(x, dtype=torch.float32, device=self.layers[0].weight.device)
+        x = x.reshape(-1, self.agent_amount * OBS_SPACE)
+        act = F.relu if self.activation is nn.ReLU else self.activation()
+        for lin in self.layers[:-1]:
+            x = act(lin(x))
+        return self.layers[-1](x)

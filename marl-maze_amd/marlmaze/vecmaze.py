@@ -104,12 +104,15 @@ class VecMaze:
                                            _lib.ptr(masks), _lib.stream_ptr()), "mm_env_reset")
         return obs, masks
 
-    def step(self, actions, auto_reset=True, obs=None, masks=None, reward=None, done=None):
+    def step(self, actions, auto_reset=True, obs=None, masks=None, reward=None, done=None, ep_stats=None):
         """Maze.step(actions) for all mazes (maze.py:74-122).
 
         actions: [n, 2, 2] int8 (move 0..4, mark 0/1) on the device.  With
-        ``auto_reset`` finished mazes are regenerated and their rows hold the
-        reset observation, as ``PPO.get_batch`` does (PPO.py:127-130).
+        ``auto_reset`` (=1/True) finished mazes are regenerated and their rows
+        hold the reset observation, as ``PPO.get_batch`` does (PPO.py:127-130);
+        ``auto_reset=2`` only queues them for ``reset_done()``.
+        ep_stats: optional [n, 2] int32 receiving (episode length, shortest
+        path length) for the mazes that finished this step.
         """
         obs = self.obs if obs is None else obs
         masks = self.masks if masks is None else masks
@@ -118,9 +121,17 @@ class VecMaze:
         if actions.dtype != torch.int8 or not actions.is_contiguous():
             actions = actions.to(torch.int8).contiguous()
         _lib.check(_lib.lib().mm_env_step(ctypes.byref(self._desc), _lib.ptr(actions), _lib.ptr(obs),
-                                          _lib.ptr(masks), _lib.ptr(reward), _lib.ptr(done),
-                                          int(bool(auto_reset)), _lib.stream_ptr()), "mm_env_step")
+                                          _lib.ptr(masks), _lib.ptr(reward), _lib.ptr(done), _lib.ptr(ep_stats),
+                                          int(auto_reset), _lib.stream_ptr()), "mm_env_step")
         return obs, masks, reward, done
+
+    def reset_done(self, obs=None, masks=None):
+        """Reset the mazes queued by the last step(auto_reset=2)."""
+        obs = self.obs if obs is None else obs
+        masks = self.masks if masks is None else masks
+        _lib.check(_lib.lib().mm_env_reset_done(ctypes.byref(self._desc), _lib.ptr(obs), _lib.ptr(masks),
+                                                _lib.stream_ptr()), "mm_env_reset_done")
+        return obs, masks
 
     # ------------------------------------------------------------------
     # host-side introspection (tests, facades, stats) -- synchronising

@@ -1,0 +1,159 @@
+"""CPU-only checks of the host side: the C ABI library loads and exports every
+declared symbol, the struct mirrors match the header, the product networks
+initialise exactly like the reference, and the data-parallel update logic
+(gloo, world size 2) equals a single-process update on the union batch."""
+import os
+import re
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from marlmaze import _lib
+from marlmaze.vecmaze import AGENT_DTYPE, MAZE_DTYPE
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "marlmaze.h")
+
+
+def _ensure_lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        from marlmaze import _build
+        _build.build()
+
+
+def test_library_exports_every_declared_symbol():
+    _ensure_lib()
+    decl = set(re.findall(r"^\s*int\s+(mm_\w+)\s*\(", open(HEADER).read(), re.M))
+    assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
+    L = _lib.lib()
+    for sym in decl:
+        assert getattr(L, sym) is not None
+    assert L.mm_version() >= 100
+    assert L.mm_layout_stride(10, 10, 0, 6, 12) == 19 * 19
+    assert L.mm_layout_stride(4, 4, 1, 12, 13) == 25 * 25
+    assert L.mm_layout_stride(30, 30, 0, 6, 12) < 0  # beyond MM_MAX_SIDE
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for sym in decl:
+        assert re.search(rf"\bT {sym}\b", nm), sym
+
+
+def test_struct_mirrors_match_header():
+    h = open(HEADER).read()
+    assert "int32_t spawn1;" in h and AGENT_DTYPE.itemsize == 32 and MAZE_DTYPE.itemsize == 32
+    assert _lib.EnvDesc.layout.offset == 40 and ctypes_size(_lib.EnvDesc) == 80
+    for name, val in (("MM_OBS_DIM", _lib.OBS_DIM), ("MM_MASK_DIM", _lib.MASK_DIM),
+                      ("MM_RNG_WORDS", _lib.RNG_WORDS), ("MM_MAX_SIDE", _lib.MAX_SIDE)):
+        assert re.search(rf"#define {name} {val}\b", h), name
+
+
+def ctypes_size(t):
+    import ctypes
+    return ctypes.sizeof(t)
+
+
+def test_product_networks_initialise_like_reference(golden):
+    from marlmaze.networks import Actor, Critic
+
+    n = golden("nets")
+    old = torch.get_num_threads()
+    torch.set_num_threads(4)  # orthogonal_ (LAPACK QR) depends on the thread count
+    try:
+        torch.manual_seed(3234)
+        actor, critic = Actor([264, 264, 264]), Critic(2, hidden_sizes=[64, 64])
+    finally:
+        torch.set_num_threads(old)
+    sd = actor.state_dict()
+    assert len(sd) == 59 and len(critic.state_dict()) == 6
+    for k, v in sd.items():
+        assert np.array_equal(v.numpy(), n["actor/" + k]), k
+    for k, v in critic.state_dict().items():
+        assert np.array_equal(v.numpy(), n["critic/" + k]), k
+    # packed-GEMM forward == reference arithmetic (CPU, tight tolerance)
+    o = torch.as_tensor(n["obs"])
+    with torch.no_grad():
+        mv, mr = actor(o.reshape(-1, 65))
+        v = critic(o)
+    np.testing.assert_allclose(mv.numpy(), n["move_logits"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(mr.numpy(), n["mark_logits"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(v.numpy(), n["values"], rtol=1e-5, atol=1e-6)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+_DP_WORKER = r"""
+import os, sys
+sys.path.insert(0, {pkg!r}); sys.path.insert(0, {repo!r})
+import numpy as np, torch
+import torch.distributed as dist
+from marlmaze.dist import DP
+from marlmaze.PPO import PPO
+rank = int(sys.argv[1]); world = 2
+os.environ.update(RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+dp = DP.from_env(backend="gloo")
+torch.set_num_threads(1)
+data = np.load(sys.argv[3])
+Bl = data["obs"].shape[0] // 2
+sl = slice(rank * Bl, (rank + 1) * Bl)
+ag = PPO(2, batch_size=2 * Bl - (2 * Bl) % 10, lr=1e-6, device="cpu", dp=dp, load=False, verbose=False, save=False)
+hist = ag.update(*(torch.as_tensor(data[k][sl]) for k in ("obs", "act", "logp", "masks", "adv", "val")),
+                 index_list=data["idx%d" % rank])
+if rank == 0:
+    np.savez(sys.argv[4], hist=hist.numpy(), **{{k: v.numpy() for k, v in ag.actor.state_dict().items()}})
+dist.destroy_process_group()
+"""
+
+
+def test_data_parallel_update_equals_single_process(tmp_path, golden):
+    """2 gloo ranks, each with half the batch and its own shuffle, give the
+    same losses/parameters as one process whose minibatches are the unions."""
+    from marlmaze.PPO import PPO
+
+    t = golden("train_small")
+    B = 640  # 2 ranks x 320
+    rng = np.random.default_rng(0)
+    data = dict(obs=t["obs"][:B], act=t["actions"][:B], logp=t["logp"][:B], masks=t["masks"][:B],
+                adv=t["advs"][:B], val=t["vals"][:B])
+    Bl = B // 2
+    idx = [rng.permutation(Bl) for _ in range(2)]
+    fx = str(tmp_path / "dp_in.npz")
+    np.savez(fx, idx0=idx[0], idx1=idx[1], **data)
+    port = str(_free_port())
+    out = str(tmp_path / "dp_out.npz")
+    script = str(tmp_path / "worker.py")
+    open(script, "w").write(_DP_WORKER.format(pkg=os.path.join(REPO, "marl-maze_amd"), repo=REPO))
+    procs = [subprocess.Popen([sys.executable, script, str(r), port, fx, out]) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    got = np.load(out)
+    # single process: minibatch k = rank0 slice k  U  rank1 slice k
+    local_bs = Bl - Bl % 5
+    mb_l = local_bs // 5
+    glob = []
+    for k in range(5):
+        glob += list(idx[0][k * mb_l:(k + 1) * mb_l]) + list(Bl + idx[1][k * mb_l:(k + 1) * mb_l])
+    torch.set_num_threads(1)
+    ag = PPO(2, batch_size=2 * local_bs, lr=1e-6, device="cpu", load=False, verbose=False, save=False)
+    hist = ag.update(*(torch.as_tensor(data[k]) for k in ("obs", "act", "logp", "masks", "adv", "val")),
+                     index_list=np.asarray(glob))
+    np.testing.assert_allclose(got["hist"][:, :2], hist.numpy()[:, :2], rtol=2e-5, atol=1e-6)
+    for k, v in ag.actor.state_dict().items():
+        np.testing.assert_allclose(got[k], v.numpy(), rtol=0, atol=3e-6)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_global_advantage_statistics(world):
+    from marlmaze.dist import DP
+
+    x = torch.randn(1000, dtype=torch.float32)
+    m, s = DP.single().global_mean_std(x)
+    assert torch.allclose(m, x.mean()) and torch.allclose(s, x.std())

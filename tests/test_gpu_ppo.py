@@ -1,0 +1,165 @@
+"""GPU parity of the PPO path: networks, log-probs, the minibatch update, a
+teacher-forced reference train() epoch, and the vectorised rollout loop.
+
+Tolerance: 1e-5 relative on losses / returns / logits (BASELINE parity bar),
+with a small absolute floor (1e-6) for values that are ~0 (the actor loss of a
+normalised advantage batch).  Parameters after Adam are compared at the scale
+of one Adam step (lr): Adam's first moments make an update lr*g/|g|, so a
+gradient that is ~0 on both sides may move a parameter by +-lr on one of them.
+"""
+import numpy as np
+import pytest
+import torch
+
+from marlmaze.PPO import PPO
+from marlmaze import ops
+from oracle import ppo as oppo
+from oracle.env import OracleEnv
+
+pytestmark = pytest.mark.gpu
+
+RTOL, ATOL = 1e-5, 1e-6
+
+
+def _agent(**kw):
+    kw.setdefault("load", False)
+    kw.setdefault("verbose", False)
+    kw.setdefault("save", False)
+    return PPO(2, **kw)
+
+
+def _load(agent, fx, prefix_a="actor/", prefix_c="critic/"):
+    agent.actor.load_state_dict({k[len(prefix_a):]: torch.as_tensor(fx[k]) for k in fx.files if k.startswith(prefix_a)})
+    agent.critic.load_state_dict({k[len(prefix_c):]: torch.as_tensor(fx[k]) for k in fx.files
+                                  if k.startswith(prefix_c)})
+
+
+def test_forward_matches_reference(golden):
+    n = golden("nets")
+    ag = _agent(n_envs=64)
+    _load(ag, n)
+    o = torch.as_tensor(n["obs"]).cuda()
+    with torch.no_grad():
+        mv, mr = ag.actor(o.reshape(-1, 65))
+        v = ag.critic(o)
+    np.testing.assert_allclose(mv.cpu().numpy(), n["move_logits"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(mr.cpu().numpy(), n["mark_logits"], rtol=RTOL, atol=ATOL)
+    np.testing.assert_allclose(v.cpu().numpy(), n["values"], rtol=RTOL, atol=ATOL)
+    mk = torch.as_tensor(n["masks"]).cuda()
+    ac = torch.as_tensor(n["actions"]).cuda()
+    with torch.no_grad():
+        for i in range(2):
+            np.testing.assert_allclose(ag.get_log_probs(i, o, ac, mk).cpu().numpy(), n[f"logp{i}"],
+                                       rtol=RTOL, atol=ATOL)
+        joint = ag.policy_logp(o, ac, mk)
+    np.testing.assert_allclose(joint.cpu().numpy(), n["logp0"] + n["logp1"], rtol=RTOL, atol=ATOL)
+
+
+def test_checkpoint_forward(golden):
+    """The shipped PPO.pth weights (as data) reproduce the reference logits."""
+    c = golden("ckpt_logits")
+    ag = _agent(n_envs=64)
+    _load(ag, c)
+    o = torch.as_tensor(c["obs"]).cuda()
+    with torch.no_grad():
+        mv, mr = ag.actor(o.reshape(-1, 65))
+        v = ag.critic(o)
+    np.testing.assert_allclose(mv.cpu().numpy(), c["move_logits"], rtol=RTOL, atol=1e-5)
+    np.testing.assert_allclose(mr.cpu().numpy(), c["mark_logits"], rtol=RTOL, atol=1e-5)
+    np.testing.assert_allclose(v.cpu().numpy(), c["values"], rtol=RTOL, atol=1e-5)
+
+
+def test_minibatch_update_matches_reference(golden):
+    n = golden("nets")
+    ag = _agent(n_envs=64, lr=0.00014)
+    _load(ag, n)
+    t = {k: torch.as_tensor(n[k]).cuda() for k in ("obs", "actions", "old_logp", "advs", "rtgs", "masks")}
+    al, cl, ga, gc = (float(x) for x in ag.minibatch_step(t["obs"], t["actions"], t["old_logp"], t["advs"],
+                                                           t["rtgs"], t["masks"]))
+    for got, ref in ((al, n["actor_loss"]), (cl, n["critic_loss"]), (ga, n["actor_gnorm"]), (gc, n["critic_gnorm"])):
+        assert abs(got - float(ref)) <= RTOL * abs(float(ref)) + ATOL, (got, float(ref))
+    for k, p in ag.actor.state_dict().items():
+        np.testing.assert_allclose(p.cpu().numpy(), n["actor_after/" + k], rtol=0, atol=2.1 * 0.00014)
+
+
+def test_train_epoch_teacher_forced(golden):
+    """The reference's recorded PPO.train() epoch (batch 600) replayed on the GPU."""
+    t = golden("train_small")
+    n = golden("nets")
+    ag = _agent(n_envs=64, batch_size=600, lr=0.00014)
+    _load(ag, n)  # nets.npz holds the seed-3234 initial weights train_small started from
+    b = [torch.as_tensor(t[k]).cuda() for k in ("obs", "actions", "logp", "masks", "advs", "vals")]
+    hist = ag.update(*b, index_list=t["idx"]).cpu().numpy()
+    np.testing.assert_allclose(hist[:, 0], t["actor_loss"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(hist[:, 1], t["critic_loss"], rtol=1e-4, atol=1e-6)
+    # first minibatch (identical start parameters): the 1e-5 bar
+    assert abs(hist[0, 0] - t["actor_loss"][0]) <= RTOL * abs(t["actor_loss"][0]) + ATOL
+    assert abs(hist[0, 1] - t["critic_loss"][0]) <= RTOL * abs(t["critic_loss"][0]) + ATOL
+    assert ag.actor_optim.param_groups[0]["lr"] == t["lr_final"]
+
+
+def test_get_gaes_api(golden):
+    g = golden("gae")
+    ag = _agent(n_envs=64)
+    for i in range(int(g["n"])):
+        vals = [torch.tensor([[float(v)]]) for v in g[f"L{i}/val"]]
+        adv = ag.get_GAEs(list(g[f"L{i}/rew"]), vals, list(g[f"L{i}/done"]))
+        assert adv.dtype == np.float64 and np.array_equal(adv, g[f"L{i}/adv"])
+
+
+def test_get_action_api():
+    ag = _agent(n_envs=64, sample_seed=3)
+    obs = [0.0] * 65
+    mask = [True, False, True, False, False, True]
+    for _ in range(20):
+        (move, mark), lp = ag.get_action(obs, mask)
+        assert move in (0, 2) and mark in (0, 1) and lp.shape == (1, 1) and torch.isfinite(lp).all()
+
+
+def test_rollout_loop_matches_oracle():
+    """Actions sampled on the GPU, replayed in the oracle: obs/masks/rewards/
+    dones of the whole rollout agree bit-exactly; GAE equals the reference
+    formula per episode fragment; stored log-probs equal a recomputation."""
+    n, T = 512, 40
+    cfg = dict(default_size=(6, 6), max_timestep=30)
+    ag = _agent(n_envs=n, horizon=T, batch_size=5 * (n * T // 5), bootstrap=False, sample_seed=5,
+                env_config=dict(cfg, seed_base=100))
+    b = ag.rollout()
+    ora = OracleEnv(n, seeds=np.arange(n, dtype=np.uint64) + np.uint64(100), **cfg)
+    oo, om = ora.reset_all()
+    obs = b["obs"].cpu().numpy()
+    masks = b["masks"].cpu().numpy().astype(bool)
+    act = b["act"].cpu().numpy()
+    assert np.array_equal(obs[0], oo) and np.array_equal(masks[0], om)
+    R = b["rew"].cpu().numpy()
+    D = b["done"].cpu().numpy().astype(bool)
+    for t in range(T):
+        assert masks[t][np.arange(n)[:, None], np.arange(2)[None, :], act[t, :, :, 0]].all(), t
+        oo, om, orw, od = ora.step_all(act[t], auto_reset=True)
+        assert np.array_equal(obs[t + 1], oo) and np.array_equal(masks[t + 1], om), t
+        assert np.array_equal(R[t], orw) and np.array_equal(D[t], od), t
+    V = b["val"].cpu().numpy()
+    A = b["adv"].cpu().numpy()
+    for col in range(0, n, 37):
+        s0, ref = 0, []
+        for t in range(T):
+            if D[t, col] or t == T - 1:
+                dd = D[s0:t + 1, col].copy()
+                dd[-1] = True
+                ref.append(oppo.gae_fp32(list(R[s0:t + 1, col].astype(np.float64)), V[s0:t + 1, col], dd))
+                s0 = t + 1
+        assert np.array_equal(A[:, col], np.concatenate(ref)), col
+    with torch.no_grad():
+        lp = ag.policy_logp(b["obs"][:T].reshape(-1, 2, 65), b["act"].reshape(-1, 2, 2).float(),
+                            b["masks"][:T].reshape(-1, 2, 6))
+    np.testing.assert_allclose(lp.cpu().numpy(), b["logp"].reshape(-1).cpu().numpy(), rtol=1e-5, atol=2e-6)
+    assert D.any()
+
+
+def test_train_runs_and_learns_something():
+    ag = _agent(n_envs=1024, horizon=8, batch_size=8190, epochs=2, sample_seed=9,
+                env_config=dict(default_size=(4, 4), max_timestep=40, seed_base=0))
+    ag.train()
+    assert len(ag.history) == 2
+    assert all(np.isfinite([h["actor_loss"], h["critic_loss"]]).all() for h in ag.history)
+    assert ag.history[-1]["episodes"] > 0
