@@ -157,6 +157,23 @@ int mm_gae(const float* reward, const float* value, const uint8_t* done, const f
 int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M, uint64_t seed,
               uint64_t offset, int8_t* actions, float* logp, float* joint_logp, void* stream);
 
+/* Actor front-end, fused (networks.py:31-34,51-82): the 23 feature embeddings
+ * (Projection; parity != 0 keeps quirk Q1, every embedding reads x[:, 0:d_i]),
+ * Q/K/V, softmax(QK^T/sqrt(10))V and the residual, for B rows of x [B, ldx]
+ * (ldx >= 65).  Weights: wp [23,20,4] (embedding i's Linear weight zero-padded
+ * to 4 inputs), bp [23,20], wq/wk [10,20], wv [20,20] (nn.Linear layout).
+ * Output h [B, 460] f32. */
+int mm_actor_front_fwd(const float* wp, const float* bp, const float* wq, const float* wk, const float* wv,
+                       const float* x, int ldx, int B, int parity, float* h, void* stream);
+
+/* Backward of mm_actor_front_fwd for upstream gradient dh [B, 460]: writes
+ * dT [B,23,20] (gradient of the embeddings), dQ, dK [B,23,10], dV [B,23,20]
+ * and the recomputed embeddings T [B,23,20]; the weight gradients are the
+ * token reductions dWq = dQ^T T, dWk = dK^T T, dWv = dV^T T, dW_i = dT_i^T x_i. */
+int mm_actor_front_bwd(const float* wp, const float* bp, const float* wq, const float* wk, const float* wv,
+                       const float* x, int ldx, int B, int parity, const float* dh, float* dT, float* dQ, float* dK,
+                       float* dV, float* T, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

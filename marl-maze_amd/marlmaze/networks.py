@@ -74,6 +74,62 @@ class m_Attention(nn.Module):
         return (t + ctx).reshape(B, FEATURE_AMOUNT * EMBEDDING_DIM)
 
 
+class _FusedFront(torch.autograd.Function):
+    """Projection + attention + residual as one HIP kernel each way (csrc/actor_front.hip).
+
+    Weight gradients are reductions over all B*23 tokens, done as GEMMs here:
+    dWq = dQ^T T, dWk = dK^T T, dWv = dV^T T, dW_i = dT_i^T x_slice_i, db_i = sum dT_i.
+    """
+
+    @staticmethod
+    def forward(ctx, x, wp, bp, wq, wk, wv, parity):
+        from . import _lib
+
+        B = x.shape[0]
+        x = x.contiguous()
+        wp, bp, wq, wk, wv = (t.contiguous() for t in (wp, bp, wq, wk, wv))
+        h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
+        _lib.check(_lib.lib().mm_actor_front_fwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
+                                                 int(parity), _lib.ptr(h), _lib.stream_ptr()),
+                   "mm_actor_front_fwd")
+        ctx.save_for_backward(x, wp, bp, wq, wk, wv)
+        ctx.parity = parity
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        from . import _lib
+
+        x, wp, bp, wq, wk, wv = ctx.saved_tensors
+        B = x.shape[0]
+        dh = dh.contiguous()
+        f32 = dict(dtype=torch.float32, device=x.device)
+        dT = torch.empty((B, FEATURE_AMOUNT, EMBEDDING_DIM), **f32)
+        dQ = torch.empty((B, FEATURE_AMOUNT, KQ_DIM), **f32)
+        dK = torch.empty((B, FEATURE_AMOUNT, KQ_DIM), **f32)
+        dV = torch.empty((B, FEATURE_AMOUNT, EMBEDDING_DIM), **f32)
+        T = torch.empty((B, FEATURE_AMOUNT, EMBEDDING_DIM), **f32)
+        _lib.check(_lib.lib().mm_actor_front_bwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
+                                                 int(ctx.parity), *(_lib.ptr(t) for t in (dh, dT, dQ, dK, dV, T)),
+                                                 _lib.stream_ptr()), "mm_actor_front_bwd")
+        Tf = T.view(-1, EMBEDDING_DIM)
+        dwq = dQ.view(-1, KQ_DIM).t().mm(Tf)
+        dwk = dK.view(-1, KQ_DIM).t().mm(Tf)
+        dwv = dV.view(-1, EMBEDDING_DIM).t().mm(Tf)
+        if ctx.parity:
+            dwp = dT.view(B, -1).t().mm(x[:, :4]).view(FEATURE_AMOUNT, EMBEDDING_DIM, 4)
+        else:
+            xs = x[:, _FIXED_IDX.to(x.device)] * _FIXED_MASK.to(x.device)  # [B, 23, 4]
+            dwp = torch.einsum("bic,bik->ick", dT, xs)
+        dbp = dT.sum(0)
+        return None, dwp, dbp, dwq, dwk, dwv, None
+
+
+_starts = np.cumsum([0] + FEATURE_DIMS[:-1])
+_FIXED_IDX = torch.as_tensor([[min(s + k, OBS_SPACE - 1) for k in range(4)] for s in _starts])
+_FIXED_MASK = torch.as_tensor([[1.0 if k < d else 0.0 for k in range(4)] for d in FEATURE_DIMS])
+
+
 class Actor(nn.Module):
     """networks.py:13-48.  forward(x) -> [move_logits [B,5], mark_logit [B,1]]."""
 
@@ -100,7 +156,14 @@ class Actor(nn.Module):
 
     def forward(self, x):
         x = torch.as_tensor(x, dtype=torch.float32, device=self.move_head.weight.device).reshape(-1, OBS_SPACE)
-        h = self.attention(self.projection(x))
+        if x.is_cuda:  # product path: fused HIP front-end (no fallback on the GPU)
+            pr = self.projection
+            wp = torch.stack([F.pad(lin.weight, (0, 4 - d)) for lin, d in zip(pr.layers, FEATURE_DIMS)])
+            bp = torch.stack([lin.bias for lin in pr.layers])
+            at = self.attention
+            h = _FusedFront.apply(x, wp, bp, at.querys.weight, at.keys.weight, at.values.weight, pr.parity_mode)
+        else:  # host reference path (CPU tests only)
+            h = self.attention(self.projection(x))
         act = F.relu if self.activation is nn.ReLU else self.activation()
         for lin in self.layers:
             h = act(lin(h))

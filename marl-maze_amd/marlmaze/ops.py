@@ -1,4 +1,10 @@
-"""Tensor-level wrappers of the rollout kernels (GAE scan, action sampler)."""
+"""Tensor-level wrappers of the rollout kernels (GAE scan, action sampler).
+
+Every tensor handed to the C ABI is held in a local variable until the call
+returns: a temporary (e.g. ``x.contiguous()`` inside the argument list) would
+be released at once, and torch's caching allocator could hand its block to
+the next temporary before the enqueued kernel has read it.
+"""
 import numpy as np
 import torch
 
@@ -11,23 +17,22 @@ def gae(reward, value, done, last_value=None, gamma=0.99, lam=0.95, adv=None, rt
     """PPO.get_GAEs (PPO.py:193-203) over time-major [T, N] tensors.
 
     reward, value: f32 [T, N]; done: u8/bool [T, N]; last_value: f32 [N] or
-    None (segment end treated like an episode end).  Returns (adv, rtg) with
+    None (every segment end is an episode end).  Returns (adv, rtg) with
     rtg = adv + value (PPO.py:46).  Bit-exact with the reference's fp32 order.
     """
     T, N = value.shape
+    r = reward.contiguous()
+    v = value.contiguous()
+    d = done.to(torch.uint8).contiguous()
+    lv = last_value.contiguous() if last_value is not None else None
     if adv is None:
-        adv = torch.empty_like(value)
+        adv = torch.empty_like(v)
     if rtg is None:
-        rtg = torch.empty_like(value)
-    if done.dtype != torch.uint8:
-        done = done.to(torch.uint8)
+        rtg = torch.empty_like(v)
     g = float(np.float32(gamma))
     gl = float(np.float32(gamma * lam))  # python float product, cast once (PPO.py:201)
-    _lib.check(_lib.lib().mm_gae(_lib.ptr(reward.contiguous()), _lib.ptr(value.contiguous()),
-                                 _lib.ptr(done.contiguous()),
-                                 _lib.ptr(last_value.contiguous() if last_value is not None else None),
-                                 int(T), int(N), g, gl, _lib.ptr(adv), _lib.ptr(rtg), _lib.stream_ptr()),
-               "mm_gae")
+    _lib.check(_lib.lib().mm_gae(_lib.ptr(r), _lib.ptr(v), _lib.ptr(d), _lib.ptr(lv), int(T), int(N), g, gl,
+                                 _lib.ptr(adv), _lib.ptr(rtg), _lib.stream_ptr()), "mm_gae")
     return adv, rtg
 
 
@@ -39,16 +44,16 @@ def sample(move_logits, mark_logits, masks, seed, offset, actions=None, logp=Non
     """
     M = move_logits.shape[0]
     dev = move_logits.device
+    ml = move_logits.contiguous()
+    kl = mark_logits.contiguous()
+    mk = masks.to(torch.uint8).contiguous()
     if actions is None:
         actions = torch.empty((M, 2), dtype=torch.int8, device=dev)
     if logp is None:
         logp = torch.empty(M, dtype=torch.float32, device=dev)
     if joint_logp is None:
         joint_logp = torch.empty((M + 1) // 2, dtype=torch.float32, device=dev)
-    if masks.dtype != torch.uint8:
-        masks = masks.to(torch.uint8)
-    _lib.check(_lib.lib().mm_sample(_lib.ptr(move_logits.contiguous()), _lib.ptr(mark_logits.contiguous()),
-                                    _lib.ptr(masks.contiguous()), int(M), int(seed) & (2**64 - 1),
+    _lib.check(_lib.lib().mm_sample(_lib.ptr(ml), _lib.ptr(kl), _lib.ptr(mk), int(M), int(seed) & (2**64 - 1),
                                     int(offset) & (2**64 - 1), _lib.ptr(actions), _lib.ptr(logp),
                                     _lib.ptr(joint_logp), _lib.stream_ptr()), "mm_sample")
     return actions, logp, joint_logp

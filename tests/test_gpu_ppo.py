@@ -163,3 +163,30 @@ def test_train_runs_and_learns_something():
     assert len(ag.history) == 2
     assert all(np.isfinite([h["actor_loss"], h["critic_loss"]]).all() for h in ag.history)
     assert ag.history[-1]["episodes"] > 0
+
+
+@pytest.mark.parametrize("parity", [True, False])
+def test_fused_front_matches_torch(parity):
+    """csrc/actor_front.hip forward+backward == the module-by-module torch path."""
+    from marlmaze.networks import Actor, _FusedFront, FEATURE_DIMS
+    import torch.nn.functional as F
+
+    torch.manual_seed(0)
+    actor = Actor([264, 264, 264], parity_mode=parity).cuda()
+    with torch.no_grad():  # non-trivial attention weights
+        for p in actor.parameters():
+            p.mul_(3.0)
+    B = 3000
+    x = torch.randn(B, 65, device="cuda")
+    dh = torch.randn(B, 460, device="cuda")
+    pr, at = actor.projection, actor.attention
+    params = [p for m in (pr, at) for p in m.parameters()]
+    href = at(pr(x))
+    gref = torch.autograd.grad(href, params, dh)
+    wp = torch.stack([F.pad(l.weight, (0, 4 - d)) for l, d in zip(pr.layers, FEATURE_DIMS)])
+    bp = torch.stack([l.bias for l in pr.layers])
+    h = _FusedFront.apply(x, wp, bp, at.querys.weight, at.keys.weight, at.values.weight, parity)
+    np.testing.assert_allclose(h.detach().cpu().numpy(), href.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)
+    g = torch.autograd.grad(h, params, dh)
+    for a, b in zip(g, gref):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-3 * b.abs().max().item())
