@@ -166,13 +166,15 @@ int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t*
 int mm_actor_front_fwd(const float* wp, const float* bp, const float* wq, const float* wk, const float* wv,
                        const float* x, int ldx, int B, int parity, float* h, void* stream);
 
-/* Backward of mm_actor_front_fwd for upstream gradient dh [B, 460]: writes
- * dT [B,23,20] (gradient of the embeddings), dQ, dK [B,23,10], dV [B,23,20]
- * and the recomputed embeddings T [B,23,20]; the weight gradients are the
- * token reductions dWq = dQ^T T, dWk = dK^T T, dWv = dV^T T, dW_i = dT_i^T x_i. */
+/* Backward of mm_actor_front_fwd for the upstream gradient dh [B, 460]: a
+ * persistent grid of `grid` workgroups, each writing one row of
+ * partial [grid, mm_actor_front_grad_len()] = its rows' weight gradients laid
+ * out as [dwq 10x20 | dwk 10x20 | dwv 20x20 | dwp 23x20x4 | dbp 23x20]; the
+ * caller sums the rows (deterministic: fixed row -> workgroup map). */
+int mm_actor_front_grad_len(void);
 int mm_actor_front_bwd(const float* wp, const float* bp, const float* wq, const float* wk, const float* wv,
-                       const float* x, int ldx, int B, int parity, const float* dh, float* dT, float* dQ, float* dK,
-                       float* dV, float* T, void* stream);
+                       const float* x, int ldx, int B, int parity, const float* dh, float* partial, int grid,
+                       void* stream);
 
 #ifdef __cplusplus
 }

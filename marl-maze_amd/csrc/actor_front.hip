@@ -3,20 +3,20 @@
 // the 23 tokens and the residual (networks.py:67-82), forward and backward.
 //
 // Why fused: per sample the front-end is a chain of 23x20 / 23x23 matrices.
-// As library calls it becomes batched GEMMs with 10..23-wide tiles (the
-// dominant cost of the PPO update before this kernel) plus [B,23,40]
-// split/cat copies.  Here one 32-lane group owns one sample, lane i = token i
-// (23 of 32 lanes active): its embedding, q, k, v stay in registers, the other
-// tokens' k and v are read from LDS as wave-wide broadcasts, the weights
-// (1.2 K floats, identical for every lane) come through the scalar cache.
-// Arithmetic is fp32 in the reference's order per element (dot products in
-// increasing index order, logits / sqrt(10), softmax = exp(x - max) / sum).
+// As library calls it becomes batched GEMMs with 10..23-wide tiles plus
+// [B,23,40] split/cat copies -- the dominant cost of the PPO update.  Here a
+// 32-lane group owns one sample, lane i = token i (23 of 32 lanes active):
+// its embedding t_i and q_i stay in registers; every token's k, v (and in the
+// backward q, P, dS, dctx) sit in LDS and are read as wave-wide broadcasts
+// with 16-byte reads; the Q/K/V weights are staged once per workgroup in LDS.
+// fp32 throughout (fmaf accumulation; the reference's op order per element:
+// logits / sqrt(10), softmax = exp(x - max) / sum).
 //
-// Forward  : x [B, 65] -> h [B, 460] (= t + softmax(q k^T / sqrt10) v, flattened)
-// Backward : dh [B, 460] -> dT [B, 23, 20] (grad of the embeddings, residual +
-//            attention paths), dQ/dK [B, 23, 10], dV [B, 23, 20] and the
-//            recomputed embeddings T [B, 23, 20]; the weight gradients are then
-//            reductions over all B*23 tokens, done as GEMMs by the caller.
+// Forward : x [B, ldx] -> h [B, 460] = t + softmax(q k^T / sqrt(10)) v
+// Backward: persistent grid; each workgroup accumulates the weight gradients
+//           of the rows it owns in registers (fixed entry -> thread map, so the
+//           sum order is deterministic) and writes ONE partial row of
+//           kGradLen floats; the caller sums the partial rows.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -25,11 +25,16 @@
 
 namespace mm {
 
-constexpr int kTok = 23;    // FEATURE_AMOUNT
-constexpr int kEmb = 20;    // EMBEDDING_DIM
-constexpr int kKq = 10;     // kq_dim
-constexpr int kPin = 4;     // max feature width (networks.py:8)
+constexpr int kTok = 23;            // FEATURE_AMOUNT
+constexpr int kEmb = 20;            // EMBEDDING_DIM
+constexpr int kKq = 10;             // kq_dim
+constexpr int kPin = 4;             // max feature width (networks.py:8)
 constexpr int kRowF = kTok * kEmb;  // 460
+constexpr float kSqrtKq = 3.16227766016838f;  // f32(np.sqrt(10)): the reference divides by it
+
+// gradient partial layout: [wq 10x20 | wk 10x20 | wv 20x20 | wp 23x20x4 | bp 23x20]
+constexpr int kGQ = 0, kGK = 200, kGV = 400, kGP = 800, kGB = 800 + kTok * kEmb * kPin;
+constexpr int kGradLen = kGB + kTok * kEmb;  // 3100
 
 __constant__ int c_dims[kTok] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 2, 2, 1, 4, 1, 1, 1, 1, 1, 1, 2};
 __constant__ int c_starts_fixed[kTok] = {0,  4,  8,  12, 16, 20, 24, 28, 32, 36, 40, 44,
@@ -43,72 +48,128 @@ struct FrontW {
     const float* wv;  // [20][20]
 };
 
-// Token embedding t_i = W_i x[s_i : s_i + d_i] + b_i  (Projection, Q1 quirk when parity)
-__device__ __forceinline__ void embed(const FrontW& W, const float* __restrict__ x, int i, bool parity,
-                                      float t[kEmb]) {
-    const int d = c_dims[i];
-    const int s = parity ? 0 : c_starts_fixed[i];
-    float xv[kPin];
-#pragma unroll
-    for (int k = 0; k < kPin; k++) xv[k] = (k < d) ? x[s + k] : 0.f;
-    const float* wi = W.wp + i * kEmb * kPin;
-#pragma unroll
-    for (int c = 0; c < kEmb; c++) {
-        float acc = 0.f;
-#pragma unroll
-        for (int k = 0; k < kPin; k++)
-            if (k < d) acc = __fadd_rn(acc, __fmul_rn(wi[c * kPin + k], xv[k]));
-        t[c] = __fadd_rn(acc, W.bp[i * kEmb + c]);
+struct WLds {  // Q/K/V weights: [40][20] = rows of wq, wk, wv
+    float w[2 * kKq + kEmb][kEmb];
+};
+
+__device__ __forceinline__ void stage_w(const FrontW& W, WLds& s) {
+    for (int e = threadIdx.x; e < (2 * kKq + kEmb) * kEmb; e += blockDim.x) {
+        const int r = e / kEmb, c = e % kEmb;
+        s.w[r][c] = r < kKq ? W.wq[e] : (r < 2 * kKq ? W.wk[e - kKq * kEmb] : W.wv[e - 2 * kKq * kEmb]);
     }
 }
 
+// x slice of token i (zero beyond d_i)
+__device__ __forceinline__ float4 xslice(const float* __restrict__ xr, int i, bool parity) {
+    const int d = c_dims[i];
+    const int s = parity ? 0 : c_starts_fixed[i];
+    return make_float4(xr[s], d > 1 ? xr[s + 1] : 0.f, d > 2 ? xr[s + 2] : 0.f, d > 3 ? xr[s + 3] : 0.f);
+}
+
+// Token embedding t_i = W_i x_i + b_i (Projection; quirk Q1 when parity)
+__device__ __forceinline__ void embed(const FrontW& W, float4 xv, int i, float t[kEmb]) {
+    const float4* wi = reinterpret_cast<const float4*>(W.wp) + i * kEmb;
+#pragma unroll
+    for (int c = 0; c < kEmb; c++) {
+        const float4 w = wi[c];
+        float acc = w.x * xv.x;
+        acc = fmaf(w.y, xv.y, acc);
+        acc = fmaf(w.z, xv.z, acc);
+        acc = fmaf(w.w, xv.w, acc);
+        t[c] = acc + W.bp[i * kEmb + c];
+    }
+}
+
+// o[a] = sum_b w[r0 + a][b] t[b]
 template <int OUT>
-__device__ __forceinline__ void matvec(const float* w, const float t[kEmb], float o[OUT]) {
+__device__ __forceinline__ void matvec(const WLds& s, int r0, const float t[kEmb], float o[OUT]) {
 #pragma unroll
     for (int a = 0; a < OUT; a++) {
+        const float4* w4 = reinterpret_cast<const float4*>(s.w[r0 + a]);
         float acc = 0.f;
 #pragma unroll
-        for (int b = 0; b < kEmb; b++) acc = __fadd_rn(acc, __fmul_rn(w[a * kEmb + b], t[b]));
+        for (int b = 0; b < kEmb / 4; b++) {
+            const float4 w = w4[b];
+            acc = fmaf(w.x, t[4 * b], acc);
+            acc = fmaf(w.y, t[4 * b + 1], acc);
+            acc = fmaf(w.z, t[4 * b + 2], acc);
+            acc = fmaf(w.w, t[4 * b + 3], acc);
+        }
         o[a] = acc;
     }
 }
 
-constexpr int kFwdRows = 8;  // samples per 256-thread workgroup
-
-// Q/K/V weights staged once per workgroup in LDS (read as broadcasts: every
-// lane of a wave reads the same word), so they do not occupy scalar registers.
-struct WLds {
-    float q[kKq * kEmb];
-    float k[kKq * kEmb];
-    float v[kEmb * kEmb];
-};
-
-__device__ __forceinline__ void stage_w(const FrontW& W, WLds& s) {
-    for (int e = threadIdx.x; e < kKq * kEmb; e += blockDim.x) {
-        s.q[e] = W.wq[e];
-        s.k[e] = W.wk[e];
+template <int N>
+__device__ __forceinline__ float dot4(const float* a, const float* __restrict__ b_lds) {  // N % 2 == 0
+    float acc = 0.f;
+    if constexpr (N % 4 == 0) {
+        const float4* b4 = reinterpret_cast<const float4*>(b_lds);
+#pragma unroll
+        for (int k = 0; k < N / 4; k++) {
+            const float4 v = b4[k];
+            acc = fmaf(a[4 * k], v.x, acc);
+            acc = fmaf(a[4 * k + 1], v.y, acc);
+            acc = fmaf(a[4 * k + 2], v.z, acc);
+            acc = fmaf(a[4 * k + 3], v.w, acc);
+        }
+    } else {
+        const float2* b2 = reinterpret_cast<const float2*>(b_lds);
+#pragma unroll
+        for (int k = 0; k < N / 2; k++) {
+            const float2 v = b2[k];
+            acc = fmaf(a[2 * k], v.x, acc);
+            acc = fmaf(a[2 * k + 1], v.y, acc);
+        }
     }
-    for (int e = threadIdx.x; e < kEmb * kEmb; e += blockDim.x) s.v[e] = W.wv[e];
+    return acc;
 }
+
+template <int N>
+__device__ __forceinline__ void axpy4(float* acc, float p, const float* __restrict__ v_lds) {  // acc += p * v
+    if constexpr (N % 4 == 0) {
+        const float4* v4 = reinterpret_cast<const float4*>(v_lds);
+#pragma unroll
+        for (int k = 0; k < N / 4; k++) {
+            const float4 v = v4[k];
+            acc[4 * k] = fmaf(p, v.x, acc[4 * k]);
+            acc[4 * k + 1] = fmaf(p, v.y, acc[4 * k + 1]);
+            acc[4 * k + 2] = fmaf(p, v.z, acc[4 * k + 2]);
+            acc[4 * k + 3] = fmaf(p, v.w, acc[4 * k + 3]);
+        }
+    } else {
+        const float2* v2 = reinterpret_cast<const float2*>(v_lds);
+#pragma unroll
+        for (int k = 0; k < N / 2; k++) {
+            const float2 v = v2[k];
+            acc[2 * k] = fmaf(p, v.x, acc[2 * k]);
+            acc[2 * k + 1] = fmaf(p, v.y, acc[2 * k + 1]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------
+constexpr int kFwdRows = 8;  // samples per 256-thread workgroup
 
 __global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __restrict__ x, int ldx, int B,
                                                    int parity, float* __restrict__ h) {
-    __shared__ float Ks[kFwdRows][kTok][kKq];
-    __shared__ float Vs[kFwdRows][kTok][kEmb];
-    __shared__ WLds Ws;
+    __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKq];
+    __shared__ __attribute__((aligned(16))) float Vs[kFwdRows][kTok][kEmb];
+    __shared__ __attribute__((aligned(16))) WLds Ws;
     stage_w(W, Ws);
     __syncthreads();
-    const int g = threadIdx.x >> 5;  // sample slot in the block
+    const int g = threadIdx.x >> 5;  // sample slot in the workgroup
     const int i = threadIdx.x & 31;  // token
     const int row = blockIdx.x * kFwdRows + g;
     const bool act = (i < kTok) && (row < B);
     float t[kEmb], q[kKq];
     if (act) {
-        embed(W, x + (size_t)row * ldx, i, parity != 0, t);
+        embed(W, xslice(x + (size_t)row * ldx, i, parity != 0), i, t);
         float k[kKq], v[kEmb];
-        matvec<kKq>(Ws.q, t, q);
-        matvec<kKq>(Ws.k, t, k);
-        matvec<kEmb>(Ws.v, t, v);
+        matvec<kKq>(Ws, 0, t, q);
+        matvec<kKq>(Ws, kKq, t, k);
+        matvec<kEmb>(Ws, 2 * kKq, t, v);
 #pragma unroll
         for (int a = 0; a < kKq; a++) Ks[g][i][a] = k[a];
 #pragma unroll
@@ -116,169 +177,238 @@ __global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __rest
     }
     __syncthreads();
     if (!act) return;
-    const float inv = 3.16227766016838f;  // f32(np.sqrt(10)): the reference divides by it
     float s[kTok];
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < kTok; j++) {
-        float acc = 0.f;
-#pragma unroll
-        for (int a = 0; a < kKq; a++) acc = __fadd_rn(acc, __fmul_rn(q[a], Ks[g][j][a]));
-        s[j] = __fdiv_rn(acc, inv);
+        s[j] = dot4<kKq>(q, Ks[g][j]) / kSqrtKq;
         mx = fmaxf(mx, s[j]);
     }
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < kTok; j++) {
-        s[j] = expf(__fsub_rn(s[j], mx));
-        sum = __fadd_rn(sum, s[j]);
+        s[j] = expf(s[j] - mx);
+        sum += s[j];
     }
     float out[kEmb];
 #pragma unroll
     for (int c = 0; c < kEmb; c++) out[c] = 0.f;
 #pragma unroll
-    for (int j = 0; j < kTok; j++) {
-        const float p = __fdiv_rn(s[j], sum);
-#pragma unroll
-        for (int c = 0; c < kEmb; c++) out[c] = __fadd_rn(out[c], __fmul_rn(p, Vs[g][j][c]));
-    }
+    for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] / sum, Vs[g][j]);
     float* o = h + (size_t)row * kRowF + i * kEmb;
 #pragma unroll
     for (int c = 0; c < kEmb; c += 4)
-        *reinterpret_cast<float4*>(o + c) = make_float4(__fadd_rn(t[c], out[c]), __fadd_rn(t[c + 1], out[c + 1]),
-                                                        __fadd_rn(t[c + 2], out[c + 2]),
-                                                        __fadd_rn(t[c + 3], out[c + 3]));
+        *reinterpret_cast<float4*>(o + c) =
+            make_float4(t[c] + out[c], t[c + 1] + out[c + 1], t[c + 2] + out[c + 2], t[c + 3] + out[c + 3]);
 }
 
-constexpr int kBwdRows = 4;  // samples per 128-thread workgroup
+// ---------------------------------------------------------------------------
+// backward (persistent, in-kernel weight-gradient reduction)
+// ---------------------------------------------------------------------------
+constexpr int kBwdRows = 4;      // samples per iteration of a 128-thread workgroup
+constexpr int kBwdThreads = 128;
+constexpr int kQkvQuads = (2 * kKq + kEmb) * (kEmb / 4);  // 200 (row a, columns 4b..4b+3) of [40 x 20]
+constexpr int kPQuads = kTok * kEmb;                      // 460 (token i, channel c) x 4 inputs
+constexpr int kQ1 = (kQkvQuads + kBwdThreads - 1) / kBwdThreads;  // 2
+constexpr int kP1 = (kPQuads + kBwdThreads - 1) / kBwdThreads;    // 4
 
-__global__ __launch_bounds__(128) void k_front_bwd(FrontW W, const float* __restrict__ x, int ldx, int B, int parity,
-                                                   const float* __restrict__ dh, float* __restrict__ dT,
-                                                   float* __restrict__ dQ, float* __restrict__ dK,
-                                                   float* __restrict__ dV, float* __restrict__ Tout) {
-    __shared__ float Qs[kBwdRows][kTok][kKq];
-    __shared__ float Ks[kBwdRows][kTok][kKq];
-    __shared__ float Vs[kBwdRows][kTok][kEmb];
-    __shared__ float Ps[kBwdRows][kTok][kTok + 1];
-    __shared__ float Ss[kBwdRows][kTok][kTok + 1];  // dS
-    __shared__ float Cs[kBwdRows][kTok][kEmb];      // dctx
-    __shared__ WLds Ws;
+struct BwdLds {
+    float Q[kBwdRows][kTok][kKq];
+    float K[kBwdRows][kTok][kKq];
+    float V[kBwdRows][kTok][kEmb];
+    float T[kBwdRows][kTok][kEmb];
+    float C[kBwdRows][kTok][kEmb];     // dctx = dh
+    float P[kBwdRows][kTok][kTok + 1];
+    float S[kBwdRows][kTok][kTok + 1];  // dS
+    float G[kBwdRows][kTok][2 * kKq + kEmb];  // [dq | dk | dv] per token
+    float D[kBwdRows][kTok][kEmb];     // dt
+    float X[kBwdRows][kTok][kPin];     // token input slices
+};
+
+__global__ __launch_bounds__(kBwdThreads) void k_front_bwd(FrontW W, const float* __restrict__ x, int ldx, int B,
+                                                           int parity, const float* __restrict__ dh,
+                                                           float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) BwdLds L;
+    __shared__ __attribute__((aligned(16))) WLds Ws;
     stage_w(W, Ws);
-    __syncthreads();
     const int g = threadIdx.x >> 5;
     const int i = threadIdx.x & 31;
-    const int row = blockIdx.x * kBwdRows + g;
-    const bool act = (i < kTok) && (row < B);
-    float t[kEmb], q[kKq], k[kKq], dctx[kEmb];
-    if (act) {
-        embed(W, x + (size_t)row * ldx, i, parity != 0, t);
-        float v[kEmb];
-        matvec<kKq>(Ws.q, t, q);
-        matvec<kKq>(Ws.k, t, k);
-        matvec<kEmb>(Ws.v, t, v);
+    // weight-gradient accumulators owned by this thread
+    float aq[kQ1][4], ap[kP1][4], ab[kP1];
 #pragma unroll
-        for (int a = 0; a < kKq; a++) {
-            Qs[g][i][a] = q[a];
-            Ks[g][i][a] = k[a];
-        }
+    for (int u = 0; u < kQ1; u++) aq[u][0] = aq[u][1] = aq[u][2] = aq[u][3] = 0.f;
 #pragma unroll
-        for (int a = 0; a < kEmb; a++) Vs[g][i][a] = v[a];
-        const float* dhi = dh + (size_t)row * kRowF + i * kEmb;
-#pragma unroll
-        for (int c = 0; c < kEmb; c += 4) {
-            const float4 d4 = *reinterpret_cast<const float4*>(dhi + c);
-            dctx[c] = d4.x;
-            dctx[c + 1] = d4.y;
-            dctx[c + 2] = d4.z;
-            dctx[c + 3] = d4.w;
-        }
-#pragma unroll
-        for (int c = 0; c < kEmb; c++) Cs[g][i][c] = dctx[c];
+    for (int u = 0; u < kP1; u++) {
+        ap[u][0] = ap[u][1] = ap[u][2] = ap[u][3] = 0.f;
+        ab[u] = 0.f;
     }
-    __syncthreads();
-    const float inv = 3.16227766016838f;
-    float dq[kKq];
-    if (act) {
-        float p[kTok];
-        float mx = -INFINITY;
+    const int iters = (B + kBwdRows - 1) / kBwdRows;
+    for (int it = blockIdx.x; it < iters; it += gridDim.x) {
+        const int row = it * kBwdRows + g;
+        const bool act = (i < kTok) && (row < B);
+        __syncthreads();  // previous iteration's readers are done with L
+        float t[kEmb], q[kKq], dctx[kEmb];
+        if (i < kTok) {
+            if (act) {
+                const float4 xv = xslice(x + (size_t)row * ldx, i, parity != 0);
+                *reinterpret_cast<float4*>(L.X[g][i]) = xv;
+                embed(W, xv, i, t);
+                float k[kKq], v[kEmb];
+                matvec<kKq>(Ws, 0, t, q);
+                matvec<kKq>(Ws, kKq, t, k);
+                matvec<kEmb>(Ws, 2 * kKq, t, v);
+                const float* dhi = dh + (size_t)row * kRowF + i * kEmb;
 #pragma unroll
-        for (int j = 0; j < kTok; j++) {
-            float acc = 0.f;
+                for (int c = 0; c < kEmb; c += 4) {
+                    const float4 d4 = *reinterpret_cast<const float4*>(dhi + c);
+                    dctx[c] = d4.x;
+                    dctx[c + 1] = d4.y;
+                    dctx[c + 2] = d4.z;
+                    dctx[c + 3] = d4.w;
+                }
 #pragma unroll
-            for (int a = 0; a < kKq; a++) acc = __fadd_rn(acc, __fmul_rn(q[a], Ks[g][j][a]));
-            p[j] = __fdiv_rn(acc, inv);
-            mx = fmaxf(mx, p[j]);
+                for (int a = 0; a < kKq; a++) {
+                    L.Q[g][i][a] = q[a];
+                    L.K[g][i][a] = k[a];
+                }
+#pragma unroll
+                for (int c = 0; c < kEmb; c++) {
+                    L.V[g][i][c] = v[c];
+                    L.T[g][i][c] = t[c];
+                    L.C[g][i][c] = dctx[c];
+                }
+            } else {  // padding rows contribute nothing to the weight gradients
+                *reinterpret_cast<float4*>(L.X[g][i]) = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int a = 0; a < kKq; a++) L.Q[g][i][a] = L.K[g][i][a] = 0.f;
+#pragma unroll
+                for (int c = 0; c < kEmb; c++) L.V[g][i][c] = L.T[g][i][c] = L.C[g][i][c] = 0.f;
+            }
         }
-        float sum = 0.f;
+        __syncthreads();
+        if (act) {
+            float p[kTok];
+            float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < kTok; j++) {
-            p[j] = expf(__fsub_rn(p[j], mx));
-            sum = __fadd_rn(sum, p[j]);
+            for (int j = 0; j < kTok; j++) {
+                p[j] = dot4<kKq>(q, L.K[g][j]) / kSqrtKq;
+                mx = fmaxf(mx, p[j]);
+            }
+            float sum = 0.f;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                p[j] = expf(p[j] - mx);
+                sum += p[j];
+            }
+            float dp[kTok];
+            float rs = 0.f;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                p[j] = p[j] / sum;
+                dp[j] = dot4<kEmb>(dctx, L.V[g][j]);  // dP_ij = dctx_i . v_j
+                rs = fmaf(dp[j], p[j], rs);
+            }
+            float dq[kKq];
+#pragma unroll
+            for (int a = 0; a < kKq; a++) dq[a] = 0.f;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                const float ds = (p[j] * (dp[j] - rs)) / kSqrtKq;  // softmax backward, then / sqrt(10)
+                L.P[g][i][j] = p[j];
+                L.S[g][i][j] = ds;
+                axpy4<kKq>(dq, ds, L.K[g][j]);
+            }
+#pragma unroll
+            for (int a = 0; a < kKq; a++) L.G[g][i][a] = dq[a];
+        } else if (i < kTok) {
+#pragma unroll
+            for (int j = 0; j < kTok; j++) L.P[g][i][j] = L.S[g][i][j] = 0.f;
+#pragma unroll
+            for (int a = 0; a < kKq; a++) L.G[g][i][a] = 0.f;
         }
-        // dP_ij = dctx_i . v_j ; softmax backward ; / sqrt10
-        float dp[kTok];
-        float rs = 0.f;
+        __syncthreads();
+        if (i < kTok) {
+            // dv_i = sum_j P_ji dctx_j ; dk_i = sum_j dS_ji q_j
+            float dv[kEmb], dk[kKq];
 #pragma unroll
-        for (int j = 0; j < kTok; j++) {
-            p[j] = __fdiv_rn(p[j], sum);
-            float acc = 0.f;
+            for (int c = 0; c < kEmb; c++) dv[c] = 0.f;
 #pragma unroll
-            for (int c = 0; c < kEmb; c++) acc = __fadd_rn(acc, __fmul_rn(dctx[c], Vs[g][j][c]));
-            dp[j] = acc;
-            rs = __fadd_rn(rs, __fmul_rn(dp[j], p[j]));
+            for (int a = 0; a < kKq; a++) dk[a] = 0.f;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                axpy4<kEmb>(dv, L.P[g][j][i], L.C[g][j]);
+                axpy4<kKq>(dk, L.S[g][j][i], L.Q[g][j]);
+            }
+#pragma unroll
+            for (int a = 0; a < kKq; a++) L.G[g][i][kKq + a] = dk[a];
+#pragma unroll
+            for (int c = 0; c < kEmb; c++) L.G[g][i][2 * kKq + c] = dv[c];
+            // dt_i = dctx_i (residual) + Wq^T dq + Wk^T dk + Wv^T dv
+            float dt[kEmb];
+#pragma unroll
+            for (int b = 0; b < kEmb; b++) dt[b] = L.C[g][i][b];
+#pragma unroll
+            for (int r = 0; r < 2 * kKq + kEmb; r++) {
+                const float gr = (r < kKq) ? L.G[g][i][r] : (r < 2 * kKq ? dk[r - kKq] : dv[r - 2 * kKq]);
+                axpy4<kEmb>(dt, gr, Ws.w[r]);
+            }
+#pragma unroll
+            for (int c = 0; c < kEmb; c++) L.D[g][i][c] = dt[c];
+        }
+        __syncthreads();
+        // weight gradients of this iteration's rows, fixed thread -> entry map
+#pragma unroll
+        for (int u = 0; u < kQ1; u++) {
+            const int e = threadIdx.x + u * kBwdThreads;  // quad over [40 x 20]
+            if (e < kQkvQuads) {
+                const int r = e / (kEmb / 4), c4 = e % (kEmb / 4);
+                for (int gg = 0; gg < kBwdRows; gg++)
+#pragma unroll
+                    for (int j = 0; j < kTok; j++) {
+                        const float gr = L.G[gg][j][r];
+                        const float4 tv = reinterpret_cast<const float4*>(L.T[gg][j])[c4];
+                        aq[u][0] = fmaf(gr, tv.x, aq[u][0]);
+                        aq[u][1] = fmaf(gr, tv.y, aq[u][1]);
+                        aq[u][2] = fmaf(gr, tv.z, aq[u][2]);
+                        aq[u][3] = fmaf(gr, tv.w, aq[u][3]);
+                    }
+            }
         }
 #pragma unroll
-        for (int a = 0; a < kKq; a++) dq[a] = 0.f;
+        for (int u = 0; u < kP1; u++) {
+            const int e = threadIdx.x + u * kBwdThreads;  // (token, channel)
+            if (e < kPQuads) {
+                const int tk = e / kEmb, c = e % kEmb;
 #pragma unroll
-        for (int j = 0; j < kTok; j++) {
-            const float ds = __fdiv_rn(__fmul_rn(p[j], __fsub_rn(dp[j], rs)), inv);
-            Ps[g][i][j] = p[j];
-            Ss[g][i][j] = ds;
-#pragma unroll
-            for (int a = 0; a < kKq; a++) dq[a] = __fadd_rn(dq[a], __fmul_rn(ds, Ks[g][j][a]));
+                for (int gg = 0; gg < kBwdRows; gg++) {
+                    const float d = L.D[gg][tk][c];
+                    const float4 xv = *reinterpret_cast<const float4*>(L.X[gg][tk]);
+                    ap[u][0] = fmaf(d, xv.x, ap[u][0]);
+                    ap[u][1] = fmaf(d, xv.y, ap[u][1]);
+                    ap[u][2] = fmaf(d, xv.z, ap[u][2]);
+                    ap[u][3] = fmaf(d, xv.w, ap[u][3]);
+                    ab[u] += d;
+                }
+            }
         }
     }
-    __syncthreads();
-    if (!act) return;
-    // dv_i = sum_j P_ji dctx_j ; dk_i = sum_j dS_ji q_j
-    float dv[kEmb], dk[kKq];
+    float* out = partial + (size_t)blockIdx.x * kGradLen;
 #pragma unroll
-    for (int c = 0; c < kEmb; c++) dv[c] = 0.f;
-#pragma unroll
-    for (int a = 0; a < kKq; a++) dk[a] = 0.f;
-#pragma unroll
-    for (int j = 0; j < kTok; j++) {
-        const float pj = Ps[g][j][i];
-        const float sj = Ss[g][j][i];
-#pragma unroll
-        for (int c = 0; c < kEmb; c++) dv[c] = __fadd_rn(dv[c], __fmul_rn(pj, Cs[g][j][c]));
-#pragma unroll
-        for (int a = 0; a < kKq; a++) dk[a] = __fadd_rn(dk[a], __fmul_rn(sj, Qs[g][j][a]));
-    }
-    // dt_i = dh_i (residual) + Wq^T dq + Wk^T dk + Wv^T dv
-    float dt[kEmb];
-#pragma unroll
-    for (int b = 0; b < kEmb; b++) {
-        float acc = dctx[b];
-#pragma unroll
-        for (int a = 0; a < kKq; a++) acc = __fadd_rn(acc, __fmul_rn(Ws.q[a * kEmb + b], dq[a]));
-#pragma unroll
-        for (int a = 0; a < kKq; a++) acc = __fadd_rn(acc, __fmul_rn(Ws.k[a * kEmb + b], dk[a]));
-#pragma unroll
-        for (int a = 0; a < kEmb; a++) acc = __fadd_rn(acc, __fmul_rn(Ws.v[a * kEmb + b], dv[a]));
-        dt[b] = acc;
-    }
-    const size_t tok = (size_t)row * kTok + i;
-#pragma unroll
-    for (int c = 0; c < kEmb; c += 4) {
-        *reinterpret_cast<float4*>(dT + tok * kEmb + c) = make_float4(dt[c], dt[c + 1], dt[c + 2], dt[c + 3]);
-        *reinterpret_cast<float4*>(dV + tok * kEmb + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
-        *reinterpret_cast<float4*>(Tout + tok * kEmb + c) = make_float4(t[c], t[c + 1], t[c + 2], t[c + 3]);
+    for (int u = 0; u < kQ1; u++) {
+        const int e = threadIdx.x + u * kBwdThreads;
+        if (e < kQkvQuads) {
+            const int r = e / (kEmb / 4), c4 = e % (kEmb / 4);
+            *reinterpret_cast<float4*>(out + kGQ + r * kEmb + 4 * c4) =
+                make_float4(aq[u][0], aq[u][1], aq[u][2], aq[u][3]);
+        }
     }
 #pragma unroll
-    for (int a = 0; a < kKq; a += 2) {
-        *reinterpret_cast<float2*>(dQ + tok * kKq + a) = make_float2(dq[a], dq[a + 1]);
-        *reinterpret_cast<float2*>(dK + tok * kKq + a) = make_float2(dk[a], dk[a + 1]);
+    for (int u = 0; u < kP1; u++) {
+        const int e = threadIdx.x + u * kBwdThreads;
+        if (e < kPQuads) {
+            *reinterpret_cast<float4*>(out + kGP + e * kPin) = make_float4(ap[u][0], ap[u][1], ap[u][2], ap[u][3]);
+            out[kGB + e] = ab[u];
+        }
     }
 }
 
@@ -297,15 +427,15 @@ extern "C" int mm_actor_front_fwd(const float* wp, const float* bp, const float*
     return (int)hipGetLastError();
 }
 
+extern "C" int mm_actor_front_grad_len(void) { return kGradLen; }
+
 extern "C" int mm_actor_front_bwd(const float* wp, const float* bp, const float* wq, const float* wk,
                                   const float* wv, const float* x, int ldx, int B, int parity, const float* dh,
-                                  float* dT, float* dQ, float* dK, float* dV, float* T, void* stream) {
-    if (!wp || !bp || !wq || !wk || !wv || !x || !dh || !dT || !dQ || !dK || !dV || !T || B < 0 ||
-        ldx < MM_OBS_DIM)
+                                  float* partial, int grid, void* stream) {
+    if (!wp || !bp || !wq || !wk || !wv || !x || !dh || !partial || B < 0 || ldx < MM_OBS_DIM || grid <= 0)
         return MM_E_ARG;
-    if (B == 0) return 0;
     FrontW W{wp, bp, wq, wk, wv};
-    hipLaunchKernelGGL(k_front_bwd, dim3((B + kBwdRows - 1) / kBwdRows), dim3(128), 0, (hipStream_t)stream, W, x,
-                       ldx, B, parity, dh, dT, dQ, dK, dV, T);
+    hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, (hipStream_t)stream, W, x, ldx, B, parity, dh,
+                       partial);
     return (int)hipGetLastError();
 }

@@ -77,8 +77,9 @@ class m_Attention(nn.Module):
 class _FusedFront(torch.autograd.Function):
     """Projection + attention + residual as one HIP kernel each way (csrc/actor_front.hip).
 
-    Weight gradients are reductions over all B*23 tokens, done as GEMMs here:
-    dWq = dQ^T T, dWk = dK^T T, dWv = dV^T T, dW_i = dT_i^T x_slice_i, db_i = sum dT_i.
+    The backward kernel reduces the weight gradients (sums over all B*23
+    tokens) inside a persistent grid into per-workgroup partial rows; one
+    torch sum over those rows finishes them.
     """
 
     @staticmethod
@@ -103,31 +104,57 @@ class _FusedFront(torch.autograd.Function):
         x, wp, bp, wq, wk, wv = ctx.saved_tensors
         B = x.shape[0]
         dh = dh.contiguous()
-        f32 = dict(dtype=torch.float32, device=x.device)
-        dT = torch.empty((B, FEATURE_AMOUNT, EMBEDDING_DIM), **f32)
-        dQ = torch.empty((B, FEATURE_AMOUNT, KQ_DIM), **f32)
-        dK = torch.empty((B, FEATURE_AMOUNT, KQ_DIM), **f32)
-        dV = torch.empty((B, FEATURE_AMOUNT, EMBEDDING_DIM), **f32)
-        T = torch.empty((B, FEATURE_AMOUNT, EMBEDDING_DIM), **f32)
-        _lib.check(_lib.lib().mm_actor_front_bwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
-                                                 int(ctx.parity), *(_lib.ptr(t) for t in (dh, dT, dQ, dK, dV, T)),
-                                                 _lib.stream_ptr()), "mm_actor_front_bwd")
-        Tf = T.view(-1, EMBEDDING_DIM)
-        dwq = dQ.view(-1, KQ_DIM).t().mm(Tf)
-        dwk = dK.view(-1, KQ_DIM).t().mm(Tf)
-        dwv = dV.view(-1, EMBEDDING_DIM).t().mm(Tf)
-        if ctx.parity:
-            dwp = dT.view(B, -1).t().mm(x[:, :4]).view(FEATURE_AMOUNT, EMBEDDING_DIM, 4)
-        else:
-            xs = x[:, _FIXED_IDX.to(x.device)] * _FIXED_MASK.to(x.device)  # [B, 23, 4]
-            dwp = torch.einsum("bic,bik->ick", dT, xs)
-        dbp = dT.sum(0)
+        L = _lib.lib()
+        glen = L.mm_actor_front_grad_len()
+        grid = max(1, min(1024, (B + 3) // 4))
+        partial = torch.empty((grid, glen), dtype=torch.float32, device=x.device)
+        _lib.check(L.mm_actor_front_bwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
+                                        int(ctx.parity), _lib.ptr(dh), _lib.ptr(partial), grid, _lib.stream_ptr()),
+                   "mm_actor_front_bwd")
+        g = partial.sum(0)
+        n_qk, n_v = KQ_DIM * EMBEDDING_DIM, EMBEDDING_DIM * EMBEDDING_DIM
+        n_p = FEATURE_AMOUNT * EMBEDDING_DIM * 4
+        dwq = g[0:n_qk].view(KQ_DIM, EMBEDDING_DIM)
+        dwk = g[n_qk:2 * n_qk].view(KQ_DIM, EMBEDDING_DIM)
+        dwv = g[2 * n_qk:2 * n_qk + n_v].view(EMBEDDING_DIM, EMBEDDING_DIM)
+        o = 2 * n_qk + n_v
+        dwp = g[o:o + n_p].view(FEATURE_AMOUNT, EMBEDDING_DIM, 4)
+        dbp = g[o + n_p:].view(FEATURE_AMOUNT, EMBEDDING_DIM)
         return None, dwp, dbp, dwq, dwk, dwv, None
 
 
-_starts = np.cumsum([0] + FEATURE_DIMS[:-1])
-_FIXED_IDX = torch.as_tensor([[min(s + k, OBS_SPACE - 1) for k in range(4)] for s in _starts])
-_FIXED_MASK = torch.as_tensor([[1.0 if k < d else 0.0 for k in range(4)] for d in FEATURE_DIMS])
+class _SplitKLinear(torch.autograd.Function):
+    """nn.Linear whose weight gradient dW = dY^T X (a reduction over all
+    M >> 10^5 rows into a 264 x 460 tile grid) runs as a split-K batched GEMM:
+    S slices of M/S rows each, then a sum over the S partial [out, in] tiles.
+    As one GEMM the reduction gets only (out/32)*(in/32) output tiles, far
+    fewer than the 256 CUs; split S ways it fills the chip."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = dy.mm(w)
+        M = x.shape[0]
+        S = 16 if M >= 16 * 4096 else 1
+        if S > 1:
+            m = M - M % S
+            dw = torch.bmm(dy[:m].view(S, m // S, -1).transpose(1, 2), x[:m].view(S, m // S, -1)).sum(0)
+            if m < M:
+                dw = dw + dy[m:].t().mm(x[m:])
+        else:
+            dw = dy.t().mm(x)
+        return dx, dw, dy.sum(0)
+
+
+def _linear(x, w, b):
+    if x.is_cuda and torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
+        return _SplitKLinear.apply(x, w, b)
+    return F.linear(x, w, b)
 
 
 class Actor(nn.Module):
@@ -166,9 +193,9 @@ class Actor(nn.Module):
             h = self.attention(self.projection(x))
         act = F.relu if self.activation is nn.ReLU else self.activation()
         for lin in self.layers:
-            h = act(lin(h))
-        heads = F.linear(h, torch.cat([self.move_head.weight, self.mark_head.weight], 0),
-                         torch.cat([self.move_head.bias, self.mark_head.bias], 0))
+            h = act(_linear(h, lin.weight, lin.bias))
+        heads = _linear(h, torch.cat([self.move_head.weight, self.mark_head.weight], 0),
+                        torch.cat([self.move_head.bias, self.mark_head.bias], 0))
         return [heads[:, :5], heads[:, 5:6]]
 
 
@@ -196,5 +223,5 @@ class Critic(nn.Module):
         x = x.reshape(-1, self.agent_amount * OBS_SPACE)
         act = F.relu if self.activation is nn.ReLU else self.activation()
         for lin in self.layers[:-1]:
-            x = act(lin(x))
-        return self.layers[-1](x)
+            x = act(_linear(x, lin.weight, lin.bias))
+        return _linear(x, self.layers[-1].weight, self.layers[-1].bias)

@@ -186,7 +186,8 @@ def test_fused_front_matches_torch(parity):
     wp = torch.stack([F.pad(l.weight, (0, 4 - d)) for l, d in zip(pr.layers, FEATURE_DIMS)])
     bp = torch.stack([l.bias for l in pr.layers])
     h = _FusedFront.apply(x, wp, bp, at.querys.weight, at.keys.weight, at.values.weight, parity)
-    np.testing.assert_allclose(h.detach().cpu().numpy(), href.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)
+    # weights x3: large attention logits amplify summation-order differences
+    np.testing.assert_allclose(h.detach().cpu().numpy(), href.detach().cpu().numpy(), rtol=1e-4, atol=2e-4)
     g = torch.autograd.grad(h, params, dh)
     for a, b in zip(g, gref):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-3 * b.abs().max().item())
