@@ -111,27 +111,130 @@ MM_HD int rel_nbrs(const View& v, int dir, int x, int y) {
     return r;
 }
 
-// Agent.get_observations (maze_agent.py:89-140) incl. get_visibility_features
-// (:188-277) and get_dead_ends (:143-185).  `s` is the observer, `q` the other
-// agent; `q_registered` = q is in maze.agent_positions (false only for agent
-// 0 inside Maze.reset, maze.py:64-71).  Writes 65 floats to o[] (stride
-// ostride) and 6 mask bytes to mk[].  Returns np.argmax(next_move_to_exit).
-template <typename OutF>
-MM_HD int observe(const View& v, Agent& s, Agent& q, bool q_registered, OutF&& out,
-                                       uint8_t* mk) {
-    // --- get_visibility_features
+// One ray of the cross-shaped neighbourhood of (x, y) in absolute direction
+// ad: every cell that the ray of get_visibility_features or the dead-end probe
+// of get_dead_ends can touch, gathered with independent (clamped,
+// unconditional) loads and kept as bitmasks.
+struct DirWin {
+    uint32_t fwd;    // bit j-1: cell j (1..5) along the ray is open (in bounds, not a wall)
+    uint32_t side;   // bit j-1: a side neighbour ((ad+1) or (ad+3)) of ray cell j (1..4) is open
+    uint32_t m2;     // bit j-1: ray cell j (1..4) holds a mark of tag 2
+    uint32_t m3;     //                                    ... of tag 3
+};
+
+MM_HD int cell_at(const View& v, int x, int y) {  // reference cell value, 1 outside the grid
+    const int cx = min(max(x, 0), v.w - 1), cy = min(max(y, 0), v.h - 1);
+    const int c = v.L[cy * v.w + cx] & 3;
+    return v.inb(x, y) ? c : 1;
+}
+
+MM_HD DirWin gather_dir(const View& v, int x, int y, int ad) {
+    const int ar = (ad + 1) & 3, al = (ad + 3) & 3;
+    DirWin w{0, 0, 0, 0};
+#pragma unroll
+    for (int j = 1; j <= 5; j++) {
+        const int cx = x + j * ddx(ad), cy = y + j * ddy(ad);
+        const int c = cell_at(v, cx, cy);
+        w.fwd |= (uint32_t)(c != 1) << (j - 1);
+        if (j <= 4) {
+            w.m2 |= (uint32_t)(c == 2) << (j - 1);
+            w.m3 |= (uint32_t)(c == 3) << (j - 1);
+            const bool so = cell_at(v, cx + ddx(ar), cy + ddy(ar)) != 1 || cell_at(v, cx + ddx(al), cy + ddy(al)) != 1;
+            w.side |= (uint32_t)so << (j - 1);
+        }
+    }
+    return w;
+}
+
+// Distance j (1..L) at which the ray from (x, y) in absolute direction ad
+// passes (tx, ty); 0 if it does not within the L visible cells.
+MM_HD int ray_hit(int x, int y, int ad, int tx, int ty, int L) {
+    int j;
+    if (ad == 0) j = (tx == x) ? y - ty : 0;
+    else if (ad == 1) j = (ty == y) ? tx - x : 0;
+    else if (ad == 2) j = (tx == x) ? ty - y : 0;
+    else j = (ty == y) ? x - tx : 0;
+    return (j >= 1 && j <= L) ? j : 0;
+}
+
+// Geometry of one relative direction d of an observation, packed in a word:
+// bits 0-2 L (visible cells), 3-5 j of the end, 6-8 j of the key, 9-11 j of
+// the other agent (0 = not on this ray), 12-14 own marks, 15-17 other marks
+// on the visible cells, 18-20 dead-end value in quarters (4 = wall next to
+// the agent, 0..3 = 1 - j/4 with j=4 -> 0 (Q12)).  Depends only on the two
+// positions, the facing and the layout -- never on the agents' knowledge --
+// so it can be computed for both agents before the order-dependent replay.
+MM_HD uint32_t summarize_dir(const View& v, int x, int y, int dir, int d, int tag, int qx, int qy, bool q_reg) {
+    const int ad = (d + dir) & 3;
+    const DirWin w = gather_dir(v, x, y, ad);
+    const int t = __builtin_ctz(~w.fwd);
+    const int L = t < 4 ? t : 4;
+    const int je = ray_hit(x, y, ad, v.ex, v.ey, L);
+    const int jk = (v.kx >= 0) ? ray_hit(x, y, ad, v.kx, v.ky, L) : 0;
+    const int ja = q_reg ? ray_hit(x, y, ad, qx, qy, L) : 0;
+    const uint32_t vis = (1u << L) - 1u;
+    const int own = __builtin_popcount((tag == 2 ? w.m2 : w.m3) & vis);
+    const int oth = __builtin_popcount((tag == 2 ? w.m3 : w.m2) & vis);
+    int dead = (w.fwd & 1u) ? 0 : 4;  // get_dead_ends (:150-181)
+    if (w.fwd & 1u) {
+#pragma unroll
+        for (int j = 1; j <= 4; j++) {
+            if (w.side >> (j - 1) & 1u) break;   // a turn: not a dead end
+            if (!(w.fwd >> j & 1u)) {           // only the way back is open
+                dead = 4 - j;
+                break;
+            }
+        }
+    }
+    return (uint32_t)L | (uint32_t)je << 3 | (uint32_t)jk << 6 | (uint32_t)ja << 9 | (uint32_t)own << 12 |
+           (uint32_t)oth << 15 | (uint32_t)dead << 18;
+}
+
+MM_HD int sum_L(uint32_t s) { return s & 7; }
+MM_HD int sum_je(uint32_t s) { return s >> 3 & 7; }
+MM_HD int sum_jk(uint32_t s) { return s >> 6 & 7; }
+MM_HD int sum_ja(uint32_t s) { return s >> 9 & 7; }
+MM_HD int sum_own(uint32_t s) { return s >> 12 & 7; }
+MM_HD int sum_oth(uint32_t s) { return s >> 15 & 7; }
+MM_HD int sum_dead(uint32_t s) { return s >> 18 & 7; }
+
+// The other agent seen on ray d at distance j (maze_agent.py:239-260).
+MM_HD void sight_agent(Agent& s, Agent& q, int d, int j, int& va, int& vad) {
+    s.tfls = 0;
+    s.olsx = q.x;
+    s.olsy = q.y;
+    if (q.f(MM_AF_KNOWS_END)) s.flags |= MM_AF_OTHER_KNOWS;
+    if (q.f(MM_AF_HAS_KEY)) s.flags |= MM_AF_TEAM_KEY;
+    vad |= 1 << q.dir;
+    va |= 1 << d;
+    if (j == 1 && s.f(MM_AF_KNOWS_END) && !q.f(MM_AF_KNOWS_END)) {
+        s.flags |= MM_AF_OTHER_KNOWS;  // route copy + push/pop (:253-257) == tree path
+        q.flags |= MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS;
+    }
+}
+
+struct Vis {
+    int va, vk, vad;  // visible agents / key per relative ray, other agent's facing (bitmasks)
+};
+
+// The order-dependent part of get_visibility_features (maze_agent.py:188-277):
+// replays, from the four direction summaries, every state change the
+// reference makes -- in its order (directions 0..3, cells in increasing j, a
+// cell's end check before its agent check) -- on the observer s and on the
+// other agent q.
+MM_HD Vis replay(const View& v, Agent& s, Agent& q, const uint32_t sum[4]) {
+    Vis r{0, 0, 0};
     s.tfls += 1;
     bool sees_end = v.is_end(s.x, s.y);
     bool sees_key = false;
-    int va = 0, vk = 0, vad = 0;
-    int own[4] = {0, 0, 0, 0}, oth[4] = {0, 0, 0, 0};
-    if (q.x == s.x && q.y == s.y) {  // co-location (:199-213), q's state may be stale (Q3)
+    if (q.x == s.x && q.y == s.y) {  // co-location (:199-213); q's state may be stale (Q3)
         s.tfls = 0;
-        va = 0xf;
-        s.olsx = q.x; s.olsy = q.y;
+        r.va = 0xf;
+        s.olsx = q.x;
+        s.olsy = q.y;
         if (q.f(MM_AF_HAS_KEY)) s.flags |= MM_AF_TEAM_KEY;
         if (q.f(MM_AF_KNOWS_END)) s.flags |= MM_AF_OTHER_KNOWS;
-        vad |= 1 << q.dir;
+        r.vad |= 1 << q.dir;
         if (s.f(MM_AF_KNOWS_END) && !q.f(MM_AF_KNOWS_END)) {  // route copy (implicit: tree path)
             s.flags |= MM_AF_OTHER_KNOWS;
             q.flags |= MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS;
@@ -139,103 +242,65 @@ MM_HD int observe(const View& v, Agent& s, Agent& q, bool q_registered, OutF&& o
     }
 #pragma unroll
     for (int d = 0; d < 4; d++) {  // rays (:215-269)
-        const int ad = (d + s.dir) & 3;
-        const int dx = ddx(ad), dy = ddy(ad);
-        int nx = s.x, ny = s.y;
-#pragma unroll
-        for (int j = 1; j <= 4; j++) {
-            nx += dx;
-            ny += dy;
-            if (!v.inb(nx, ny)) break;
-            const int c = v.type(nx, ny);
-            if (c == 1) break;
-            if (v.is_end(nx, ny)) {
-                s.flags |= MM_AF_KNOWS_END;
-                sees_end = true;
-                if (s.exit_len == -1) s.exit_len = j;  // route := [ad]*j == tree path
-            }
-            if (nx == v.kx && ny == v.ky) {
-                sees_key = true;
-                vk |= 1 << d;
-            }
-            if (q_registered && q.x == nx && q.y == ny) {
-                s.tfls = 0;
-                s.olsx = q.x; s.olsy = q.y;
-                if (q.f(MM_AF_KNOWS_END)) s.flags |= MM_AF_OTHER_KNOWS;
-                if (q.f(MM_AF_HAS_KEY)) s.flags |= MM_AF_TEAM_KEY;
-                vad |= 1 << q.dir;
-                va |= 1 << d;
-                if (j == 1 && s.f(MM_AF_KNOWS_END) && !q.f(MM_AF_KNOWS_END)) {
-                    s.flags |= MM_AF_OTHER_KNOWS;  // copy + push/pop (:253-257) == tree path
-                    q.flags |= MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS;
-                }
-            }
-            if (c == s.tag) own[d]++;
-            else if (c > 1) oth[d]++;
-            // update_maze_minmax (:313-328)
-            if (ad == 0 && ny < s.miny) s.miny = ny;
-            else if (ad == 1 && nx > s.maxx) s.maxx = nx;
-            else if (ad == 2 && ny > s.maxy) s.maxy = ny;
-            else if (ad == 3 && nx < s.minx) s.minx = nx;
+        const uint32_t sm = sum[d];
+        const int L = sum_L(sm), je = sum_je(sm), jk = sum_jk(sm), ja = sum_ja(sm);
+        const bool agent_first = ja && je && ja < je;
+        if (ja && agent_first) sight_agent(s, q, d, ja, r.va, r.vad);
+        if (je) {
+            s.flags |= MM_AF_KNOWS_END;
+            sees_end = true;
+            if (s.exit_len == -1) s.exit_len = je;  // route := [ad]*j == tree path
+        }
+        if (jk) {
+            sees_key = true;
+            r.vk |= 1 << d;
+        }
+        if (ja && !agent_first) sight_agent(s, q, d, ja, r.va, r.vad);
+        if (L) {  // update_maze_minmax (:313-328): the farthest visible cell decides
+            const int ad = (d + s.dir) & 3;
+            if (ad == 0) s.miny = min(s.miny, s.y - L);
+            else if (ad == 1) s.maxx = max(s.maxx, s.x + L);
+            else if (ad == 2) s.maxy = max(s.maxy, s.y + L);
+            else s.minx = min(s.minx, s.x - L);
         }
     }
     s.set(MM_AF_SEES_END, sees_end);
     s.set(MM_AF_SEES_KEY, sees_key);
+    return r;
+}
+
+// Observation vector (maze_agent.py:91-130) and action mask (:132-139) of s
+// after its replay.  out(i, value) receives the 65 elements; only elements
+// i in [lo, hi) are produced (lets 2..4 lanes share one agent's row).
+// Returns np.argmax(next_move_to_exit).
+template <typename OutF>
+MM_HD int emit(const View& v, const Agent& s, const Vis& r, const uint32_t sum[4], OutF&& out, uint8_t* mk,
+               int lo = 0, int hi = kObs) {
+    auto put = [&](int i, float x) {
+        if (i >= lo && i < hi) out(i, x);
+    };
     int west = s.maxx - s.minx, hest = s.maxy - s.miny;  // update_maze_dims (:330-336)
     if (west == 0) west = 1;
     if (hest == 0) hest = 1;
-
-    // --- get_dead_ends
-    const int nb = rel_nbrs(v, s.dir, s.x, s.y);
-    int dead_q[4];  // dead-end value in quarters: 4 = wall, 0..3 = 1 - j/4 (j=4 -> 0, Q12)
-    int mmask = nb;
 #pragma unroll
-    for (int d = 0; d < 4; d++) {
-        dead_q[d] = (nb >> d & 1) ? 0 : 4;
-        if (!(nb >> d & 1)) continue;
-        const int ad = (d + s.dir) & 3;
-        const int dx = ddx(ad), dy = ddy(ad);
-        int nx = s.x, ny = s.y;
+    for (int i = 0; i < 4; i++) put(0 + i, (i == s.dir) ? 1.f : 0.f);
 #pragma unroll
-        for (int j = 1; j <= 4; j++) {
-            nx += dx;
-            ny += dy;
-            const int n2 = rel_nbrs(v, s.dir, nx, ny);
-            if ((n2 >> ((d + 1) & 3) & 1) || (n2 >> ((d + 3) & 3) & 1)) break;
-            if (__builtin_popcount((unsigned)n2) == 1) {
-                dead_q[d] = 4 - j;
-                break;
-            } else if (!(n2 >> d & 1)) {
-                break;
-            }
-        }
-    }
-    if (!sees_end && !sees_key) {
-        mmask = 0;
+    for (int i = 0; i < 4; i++) put(4 + i, (float)sum_dead(sum[i]) * 0.25f);
 #pragma unroll
-        for (int d = 0; d < 4; d++) mmask |= (dead_q[d] == 0) ? (1 << d) : 0;
-    }
-
-    // --- observation vector (:91-130)
+    for (int i = 0; i < 4; i++) put(8 + i, (float)sum_own(sum[i]) * 0.25f);
 #pragma unroll
-    for (int i = 0; i < 4; i++) out(0 + i, (i == s.dir) ? 1.f : 0.f);
+    for (int i = 0; i < 4; i++) put(12 + i, (float)sum_oth(sum[i]) * 0.25f);
 #pragma unroll
-    for (int i = 0; i < 4; i++) out(4 + i, (float)dead_q[i] * 0.25f);
+    for (int i = 0; i < 4; i++) put(16 + i, (r.va >> i & 1) ? 1.f : 0.f);
 #pragma unroll
-    for (int i = 0; i < 4; i++) out(8 + i, (float)own[i] * 0.25f);
+    for (int i = 0; i < 4; i++) put(20 + i, (r.vad >> i & 1) ? 1.f : 0.f);
 #pragma unroll
-    for (int i = 0; i < 4; i++) out(12 + i, (float)oth[i] * 0.25f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) out(16 + i, (va >> i & 1) ? 1.f : 0.f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) out(20 + i, (vad >> i & 1) ? 1.f : 0.f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) out(24 + i, (vk >> i & 1) ? 1.f : 0.f);
+    for (int i = 0; i < 4; i++) put(24 + i, (r.vk >> i & 1) ? 1.f : 0.f);
 #pragma unroll
     for (int slot = 0; slot < 4; slot++) {  // get_memory (:289-294)
         const int mv = (int)(int8_t)((s.mem >> (8 * slot)) & 0xff);
 #pragma unroll
-        for (int k = 0; k < 4; k++) out(28 + 4 * slot + k, (mv == k) ? 1.f : 0.f);
+        for (int k = 0; k < 4; k++) put(28 + 4 * slot + k, (mv == k) ? 1.f : 0.f);
     }
     int lm = 0;  // get_direction_from (:297-311)
     if (s.f(MM_AF_HAS_MARK)) {
@@ -249,36 +314,61 @@ MM_HD int observe(const View& v, Agent& s, Agent& q, bool q_registered, OutF&& o
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) out(44 + i, (lm >> i & 1) ? 1.f : 0.f);
+    for (int i = 0; i < 4; i++) put(44 + i, (lm >> i & 1) ? 1.f : 0.f);
     // Python true division of ints in fp64, then float32 (PPO.py:144)
-    out(48, (float)((double)(s.x - s.minx) / (double)west));
-    out(49, (float)((double)(s.maxy - s.y) / (double)hest));
-    out(50, (float)((double)(s.olsx - s.minx) / (double)west));
-    out(51, (float)((double)(s.maxy - s.olsy) / (double)hest));
-    out(52, sees_end ? 1.f : 0.f);
+    if (lo <= 51 && hi > 48) {
+        put(48, (float)((double)(s.x - s.minx) / (double)west));
+        put(49, (float)((double)(s.maxy - s.y) / (double)hest));
+        put(50, (float)((double)(s.olsx - s.minx) / (double)west));
+        put(51, (float)((double)(s.maxy - s.olsy) / (double)hest));
+    }
+    put(52, s.f(MM_AF_SEES_END) ? 1.f : 0.f);
     int nme_arg = 0, nme = 0xf;  // next_move_to_exit (:113-118)
     if (s.f(MM_AF_KNOWS_END) && !v.is_end(s.x, s.y)) {
         nme_arg = (v.tdir(s.x, s.y) - s.dir) & 3;
         nme = 1 << nme_arg;
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) out(53 + i, (nme >> i & 1) ? 1.f : 0.f);
-    out(57, s.exit_len < 40 ? (float)((double)s.exit_len / 40.0) : 1.f);
-    out(58, s.f(MM_AF_OTHER_KNOWS) ? 1.f : 0.f);
-    out(59, s.f(MM_AF_HAS_KEY) ? 1.f : 0.f);
-    out(60, s.f(MM_AF_TEAM_KEY) ? 1.f : 0.f);
-    out(61, s.tfls < 40 ? (float)((double)s.tfls / 40.0) : 1.f);
-    out(62, (float)((double)v.t / (double)v.max_t));
-    out(63, s.tag == 2 ? 1.f : 0.f);
-    out(64, s.tag == 3 ? 1.f : 0.f);
-
-    // --- action mask (:132-139)
-    if (vk) mmask = vk & (-vk);  // one-hot at np.argmax(visible_key)
+    for (int i = 0; i < 4; i++) put(53 + i, (nme >> i & 1) ? 1.f : 0.f);
+    if (hi > 57) {
+        put(57, s.exit_len < 40 ? (float)((double)s.exit_len / 40.0) : 1.f);
+        put(58, s.f(MM_AF_OTHER_KNOWS) ? 1.f : 0.f);
+        put(59, s.f(MM_AF_HAS_KEY) ? 1.f : 0.f);
+        put(60, s.f(MM_AF_TEAM_KEY) ? 1.f : 0.f);
+        put(61, s.tfls < 40 ? (float)((double)s.tfls / 40.0) : 1.f);
+        put(62, (float)((double)v.t / (double)v.max_t));
+        put(63, s.tag == 2 ? 1.f : 0.f);
+        put(64, s.tag == 3 ? 1.f : 0.f);
+    }
+    if (mk) {  // --- action mask (:132-139)
+        int nb = 0, mmask = 0;
 #pragma unroll
-    for (int i = 0; i < 4; i++) mk[i] = (uint8_t)(mmask >> i & 1);
-    mk[4] = (uint8_t)(va != 0 && s.x == v.ex && s.x == v.ey);  // (x, x) == end (Q2)
-    mk[5] = (uint8_t)(v.type(s.x, s.y) != s.tag);
+        for (int d = 0; d < 4; d++) {
+            nb |= (sum_dead(sum[d]) != 4) << d;  // open neighbour (get_neighbors, relative)
+            mmask |= (sum_dead(sum[d]) == 0) << d;
+        }
+        if (s.f(MM_AF_SEES_END) || s.f(MM_AF_SEES_KEY)) mmask = nb;
+        if (r.vk) mmask = r.vk & (-r.vk);  // one-hot at np.argmax(visible_key)
+#pragma unroll
+        for (int i = 0; i < 4; i++) mk[i] = (uint8_t)(mmask >> i & 1);
+        mk[4] = (uint8_t)(r.va != 0 && s.x == v.ex && s.x == v.ey);  // (x, x) == end (Q2)
+        mk[5] = (uint8_t)(v.type(s.x, s.y) != s.tag);
+    }
     return nme_arg;
+}
+
+// Agent.get_observations (maze_agent.py:89-140) incl. get_visibility_features
+// (:188-277) and get_dead_ends (:143-185), one thread.  `s` is the observer,
+// `q` the other agent; `q_registered` = q is in maze.agent_positions (false
+// only for agent 0 inside Maze.reset, maze.py:64-71).  Returns
+// np.argmax(next_move_to_exit).
+template <typename OutF>
+MM_HD int observe(const View& v, Agent& s, Agent& q, bool q_registered, OutF&& out, uint8_t* mk) {
+    uint32_t sum[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) sum[d] = summarize_dir(v, s.x, s.y, s.dir, d, s.tag, q.x, q.y, q_registered);
+    const Vis r = replay(v, s, q, sum);
+    return emit(v, s, r, sum, out, mk);
 }
 
 // single_agent_step (maze.py:124-163).  Returns 1 if this agent picked up the

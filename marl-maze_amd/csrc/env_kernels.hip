@@ -9,12 +9,12 @@
 //   k_reset_obs  one thread per reset maze: agent resets and the two reset
 //            observations in the reference's order (maze.py:64-71: agent 0
 //            observes while agent 1 still holds its previous state, Q3).
-//   k_step   one thread per maze, 64 mazes per workgroup: Maze.step()
-//            (maze.py:74-122).  The workgroup's 64 layouts are one
-//            contiguous HBM range and are staged into LDS with 16-byte
-//            coalesced loads; observations and masks are staged in LDS and
-//            written back as contiguous 16-byte stores.  Finished mazes are
-//            appended to a done list that k_reset consumes (PPO.py:127-130).
+//   k_step   four lanes per maze, 32 mazes per workgroup: Maze.step()
+//            (maze.py:74-122).  The workgroup's 32 layouts are one contiguous
+//            HBM range, staged into LDS with 16-byte coalesced loads; each
+//            lane gathers two rays of one agent's neighbourhood as bitmasks.
+//            Finished mazes are appended to a done list that k_reset consumes
+//            (PPO.py:127-130).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -342,102 +342,125 @@ __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __res
 // ---------------------------------------------------------------------------
 // step (one thread per maze)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kMPB) void k_step(mm_env_t env, const int8_t* __restrict__ act, float* __restrict__ obs,
-                                               uint8_t* __restrict__ masks, float* __restrict__ reward,
-                                               uint8_t* __restrict__ done, int32_t* __restrict__ ep_stats,
-                                               int list_done) {
+// Four lanes per maze: lane q = 2a + h works on agent a's relative
+// directions 2h and 2h+1.  The cheap order-dependent work (moves, the replay
+// of both observations, reward) is done redundantly by all four lanes, so no
+// state has to be exchanged except the eight direction summaries (shuffles).
+constexpr int kLanes = 4;
+constexpr int kMPB4 = 32;  // mazes per 128-thread workgroup
+
+__global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8_t* __restrict__ act,
+                                                        float* __restrict__ obs, uint8_t* __restrict__ masks,
+                                                        float* __restrict__ reward, uint8_t* __restrict__ done,
+                                                        int32_t* __restrict__ ep_stats, int list_done) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int stride = env.layout_stride;
-    const int lay_bytes = (kMPB * stride + 15) & ~15;
-    uint8_t* Ls = smem;
-    float* Os = reinterpret_cast<float*>(smem + lay_bytes);  // [kMPB][2][65]
-    uint8_t* Ms = reinterpret_cast<uint8_t*>(Os + kMPB * 2 * kObs);  // [kMPB][2][6]
-
-    const int m0 = blockIdx.x * kMPB;
-    const int nb = min(kMPB, env.n - m0);
-    copy_in(Ls, env.layout + (size_t)m0 * stride, nb * stride);
-    __syncthreads();
-
-    const int i = threadIdx.x;
-    const int m = m0 + i;
-    if (i < nb) {
-        mm_maze_t mz = env.mazes[m];
-        View v;
-        v.L = Ls + i * stride;
-        v.w = mz.w; v.h = mz.h; v.ex = mz.ex; v.ey = mz.ey; v.kx = mz.kx; v.ky = mz.ky;
-        v.max_t = env.max_timestep;
-        Agent a0 = load_agent(env.agents[2 * m], 2);
-        Agent a1 = load_agent(env.agents[2 * m + 1], 3);
-        const char4 ac = reinterpret_cast<const char4*>(act)[m];
-        uint32_t status = mz.status;
-        uint8_t* gl = env.layout + (size_t)m * stride;
-        // maze.py:75-90
-        mz.t += 1;
-        v.t = mz.t;
-        int first_key = agent_step(v, a0, ac.x, ac.y, gl, status);
-        int have_key = a0.f(MM_AF_HAS_KEY);
-        first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
-        have_key += a1.f(MM_AF_HAS_KEY);
-        // maze.py:99-113
-        float* o = Os + i * 2 * kObs;
-        uint8_t* mk = Ms + i * 2 * kMask;
-        const int am0 = observe(v, a0, a1, true, [&](int k, float x) { o[k] = x; }, mk);
-        bool exit_ready = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
-        const int am1 = observe(v, a1, a0, true, [&](int k, float x) { o[kObs + k] = x; }, mk + kMask);
-        exit_ready = exit_ready && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
-        if (exit_ready) {
-            const Agent* ags[2] = {&a0, &a1};
-            const int ams[2] = {am0, am1};
-#pragma unroll
-            for (int q = 0; q < 2; q++) {
-                uint8_t* mq = mk + q * kMask;
-                if (!v.is_end(ags[q]->x, ags[q]->y)) {
-#pragma unroll
-                    for (int d = 0; d < 4; d++) mq[d] = (uint8_t)(d == ams[q]);
-                } else {
-                    mq[0] = mq[1] = mq[2] = mq[3] = 0;
-                    mq[4] = 1;
-                }
-            }
-        }
-        // reward / done :115-121
-        float r = first_key ? 0.5f * first_key : 0.f;
-        uint8_t dn = 0;
-        if (have_key && a0.x == a1.x && a0.y == a1.y && v.is_end(a0.x, a0.y)) {
-            r = 1.f;
-            dn = 1;
-        } else if (mz.t >= env.max_timestep) {
-            dn = 1;
-        }
-        reward[m] = r;
-        done[m] = dn;
-        if (ep_stats)  // (episode length, shortest_path_len) of an episode that ended here (PPO.py:129,131)
-            reinterpret_cast<int2*>(ep_stats)[m] = dn ? make_int2(mz.t, mz.path_len) : make_int2(0, 0);
-        mz.kx = (int8_t)v.kx;
-        mz.ky = (int8_t)v.ky;
-        mz.status = (uint16_t)status;
-        if (dn) {
-            mz.episodes += 1;
-            mz.last_len = mz.t;
-            mz.last_path = mz.path_len;
-            if (list_done) {
-                const int pos = atomicAdd(&env.work[0], 1);
-                if (pos < env.n) env.work[kListOff + pos] = m;  // (queue not drained by the caller: ignore)
-            }
-        }
-        env.mazes[m] = mz;
-        env.agents[2 * m] = pack_agent(a0);
-        env.agents[2 * m + 1] = pack_agent(a1);
+    const int m0 = blockIdx.x * kMPB4;
+    const int nb = min(kMPB4, env.n - m0);
+    const int lm = threadIdx.x >> 2;  // maze within the workgroup
+    const int q = threadIdx.x & 3;    // lane within the maze
+    const int a = q >> 1, h = q & 1;
+    const int m = m0 + lm;
+    const bool valid = lm < nb;
+    // per-maze state loads are issued before the layout staging barrier
+    mm_maze_t mz{};
+    mm_agent_t g0{}, g1{};
+    char4 ac{};
+    if (valid) {
+        mz = env.mazes[m];
+        g0 = env.agents[2 * m];
+        g1 = env.agents[2 * m + 1];
+        ac = reinterpret_cast<const char4*>(act)[m];
     }
+    copy_in(smem, env.layout + (size_t)m0 * stride, nb * stride);
     __syncthreads();
-    copy_out(reinterpret_cast<uint8_t*>(obs + (size_t)m0 * 2 * kObs), reinterpret_cast<const uint8_t*>(Os),
-             nb * 2 * kObs * 4);
-    copy_out(masks + (size_t)m0 * 2 * kMask, Ms, nb * 2 * kMask);
+    if (!valid) return;
+    View v;
+    v.L = smem + lm * stride;
+    v.w = mz.w; v.h = mz.h; v.ex = mz.ex; v.ey = mz.ey; v.kx = mz.kx; v.ky = mz.ky;
+    v.max_t = env.max_timestep;
+    Agent a0 = load_agent(g0, 2);
+    Agent a1 = load_agent(g1, 3);
+    uint32_t status = mz.status;
+    uint8_t* gl = (q == 0) ? env.layout + (size_t)m * stride : nullptr;
+    // maze.py:75-90 (the four lanes write identical mark bytes into LDS)
+    mz.t += 1;
+    v.t = mz.t;
+    int first_key = agent_step(v, a0, ac.x, ac.y, gl, status);
+    const int have_key0 = a0.f(MM_AF_HAS_KEY);
+    first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
+    const int have_key = have_key0 + a1.f(MM_AF_HAS_KEY);
+    // geometry of this lane's two directions of agent a
+    const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
+    const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
+    const uint32_t sB = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + 1, me0.tag, ot0.x, ot0.y, true);
+    const int base = (threadIdx.x & 63) & ~3;
+    uint32_t sum0[4], sum1[4];
+    sum0[0] = __shfl(sA, base + 0);
+    sum0[1] = __shfl(sB, base + 0);
+    sum0[2] = __shfl(sA, base + 1);
+    sum0[3] = __shfl(sB, base + 1);
+    sum1[0] = __shfl(sA, base + 2);
+    sum1[1] = __shfl(sB, base + 2);
+    sum1[2] = __shfl(sA, base + 3);
+    sum1[3] = __shfl(sB, base + 3);
+    // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1
+    const Vis r0 = replay(v, a0, a1, sum0);
+    const Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
+    const bool ready0 = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
+    const Vis r1 = replay(v, a1, a0, sum1);
+    const bool exit_ready = ready0 && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
+    // this lane's half of agent a's observation row; lane h == 0 writes the mask
+    const Agent me = a ? a1 : a0_obs;
+    const Vis rm = a ? r1 : r0;
+    uint32_t sm[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) sm[d] = a ? sum1[d] : sum0[d];
+    float* orow = obs + (size_t)(2 * m + a) * kObs;
+    uint8_t* mk = masks + (size_t)(2 * m + a) * kMask;
+    const int am = emit(v, me, rm, sm, [&](int i, float x) { orow[i] = x; }, h == 0 ? mk : nullptr,
+                        h == 0 ? 0 : 33, h == 0 ? 33 : kObs);
+    if (h == 0 && exit_ready) {  // maze.py:107-113
+        if (!v.is_end(me.x, me.y)) {
+#pragma unroll
+            for (int d = 0; d < 4; d++) mk[d] = (uint8_t)(d == am);
+        } else {
+            mk[0] = mk[1] = mk[2] = mk[3] = 0;
+            mk[4] = 1;
+        }
+    }
+    if (q != 0) return;
+    // reward / done (maze.py:115-121) and state write-back
+    float r = first_key ? 0.5f * first_key : 0.f;
+    uint8_t dn = 0;
+    if (have_key && a0.x == a1.x && a0.y == a1.y && v.is_end(a0.x, a0.y)) {
+        r = 1.f;
+        dn = 1;
+    } else if (mz.t >= env.max_timestep) {
+        dn = 1;
+    }
+    reward[m] = r;
+    done[m] = dn;
+    if (ep_stats)  // (episode length, shortest_path_len) of an episode that ended here (PPO.py:129,131)
+        reinterpret_cast<int2*>(ep_stats)[m] = dn ? make_int2(mz.t, mz.path_len) : make_int2(0, 0);
+    mz.kx = (int8_t)v.kx;
+    mz.ky = (int8_t)v.ky;
+    mz.status = (uint16_t)status;
+    if (dn) {
+        mz.episodes += 1;
+        mz.last_len = mz.t;
+        mz.last_path = mz.path_len;
+        if (list_done) {
+            const int pos = atomicAdd(&env.work[0], 1);
+            if (pos < env.n) env.work[kListOff + pos] = m;  // (queue not drained by the caller: ignore)
+        }
+    }
+    env.mazes[m] = mz;
+    env.agents[2 * m] = pack_agent(a0);
+    env.agents[2 * m + 1] = pack_agent(a1);
 }
 
-inline size_t step_lds_bytes(int stride) {
-    return (size_t)((kMPB * stride + 15) & ~15) + (size_t)kMPB * 2 * kObs * 4 + (size_t)kMPB * 2 * kMask;
-}
+inline size_t step_lds_bytes(int stride) { return (size_t)((kMPB4 * stride + 15) & ~15); }
 
 inline int check_env(const mm_env_t* env) {
     if (!env || env->n <= 0 || !env->layout || !env->agents || !env->mazes || !env->rng || !env->work) return MM_E_ARG;
@@ -497,8 +520,9 @@ extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* ob
     if (auto_reset < 0 || auto_reset > 2) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
     const size_t lds = step_lds_bytes(env->layout_stride);
-    const int grid = (env->n + kMPB - 1) / kMPB;
-    hipLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB), lds, s, *env, actions, obs, masks, reward, done, ep_stats,
+    const int grid = (env->n + kMPB4 - 1) / kMPB4;
+    hipLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB4 * kLanes), lds, s, *env, actions, obs, masks, reward, done,
+                       ep_stats,
                        auto_reset ? 1 : 0);
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
