@@ -270,37 +270,33 @@ MM_HD Vis replay(const View& v, Agent& s, Agent& q, const uint32_t sum[4]) {
 }
 
 // Observation vector (maze_agent.py:91-130) and action mask (:132-139) of s
-// after its replay.  out(i, value) receives the 65 elements; only elements
-// i in [lo, hi) are produced (lets 2..4 lanes share one agent's row).
+// after its replay, computed unconditionally into o[65] / mk[6] (registers).
 // Returns np.argmax(next_move_to_exit).
-template <typename OutF>
-MM_HD int emit(const View& v, const Agent& s, const Vis& r, const uint32_t sum[4], OutF&& out, uint8_t* mk,
-               int lo = 0, int hi = kObs) {
-    auto put = [&](int i, float x) {
-        if (i >= lo && i < hi) out(i, x);
-    };
+//
+// The reference divides small Python ints in fp64 and the tensor holds the
+// float32 of the quotient (PPO.py:144).  Both operands are integers below
+// 2^24, exactly representable in f32, and 53 >= 2*24 + 2, so the correctly
+// rounded f32 division gives the same float as fp64-then-round.
+MM_HD int build_obs(const View& v, const Agent& s, const Vis& r, const uint32_t sum[4], float o[kObs],
+                    uint8_t mk[kMask]) {
     int west = s.maxx - s.minx, hest = s.maxy - s.miny;  // update_maze_dims (:330-336)
     if (west == 0) west = 1;
     if (hest == 0) hest = 1;
 #pragma unroll
-    for (int i = 0; i < 4; i++) put(0 + i, (i == s.dir) ? 1.f : 0.f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) put(4 + i, (float)sum_dead(sum[i]) * 0.25f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) put(8 + i, (float)sum_own(sum[i]) * 0.25f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) put(12 + i, (float)sum_oth(sum[i]) * 0.25f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) put(16 + i, (r.va >> i & 1) ? 1.f : 0.f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) put(20 + i, (r.vad >> i & 1) ? 1.f : 0.f);
-#pragma unroll
-    for (int i = 0; i < 4; i++) put(24 + i, (r.vk >> i & 1) ? 1.f : 0.f);
+    for (int i = 0; i < 4; i++) {
+        o[0 + i] = (i == s.dir) ? 1.f : 0.f;
+        o[4 + i] = (float)sum_dead(sum[i]) * 0.25f;
+        o[8 + i] = (float)sum_own(sum[i]) * 0.25f;
+        o[12 + i] = (float)sum_oth(sum[i]) * 0.25f;
+        o[16 + i] = (r.va >> i & 1) ? 1.f : 0.f;
+        o[20 + i] = (r.vad >> i & 1) ? 1.f : 0.f;
+        o[24 + i] = (r.vk >> i & 1) ? 1.f : 0.f;
+    }
 #pragma unroll
     for (int slot = 0; slot < 4; slot++) {  // get_memory (:289-294)
         const int mv = (int)(int8_t)((s.mem >> (8 * slot)) & 0xff);
 #pragma unroll
-        for (int k = 0; k < 4; k++) put(28 + 4 * slot + k, (mv == k) ? 1.f : 0.f);
+        for (int k = 0; k < 4; k++) o[28 + 4 * slot + k] = (mv == k) ? 1.f : 0.f;
     }
     int lm = 0;  // get_direction_from (:297-311)
     if (s.f(MM_AF_HAS_MARK)) {
@@ -314,46 +310,40 @@ MM_HD int emit(const View& v, const Agent& s, const Vis& r, const uint32_t sum[4
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) put(44 + i, (lm >> i & 1) ? 1.f : 0.f);
-    // Python true division of ints in fp64, then float32 (PPO.py:144)
-    if (lo <= 51 && hi > 48) {
-        put(48, (float)((double)(s.x - s.minx) / (double)west));
-        put(49, (float)((double)(s.maxy - s.y) / (double)hest));
-        put(50, (float)((double)(s.olsx - s.minx) / (double)west));
-        put(51, (float)((double)(s.maxy - s.olsy) / (double)hest));
-    }
-    put(52, s.f(MM_AF_SEES_END) ? 1.f : 0.f);
+    for (int i = 0; i < 4; i++) o[44 + i] = (lm >> i & 1) ? 1.f : 0.f;
+    o[48] = __fdiv_rn((float)(s.x - s.minx), (float)west);
+    o[49] = __fdiv_rn((float)(s.maxy - s.y), (float)hest);
+    o[50] = __fdiv_rn((float)(s.olsx - s.minx), (float)west);
+    o[51] = __fdiv_rn((float)(s.maxy - s.olsy), (float)hest);
+    o[52] = s.f(MM_AF_SEES_END) ? 1.f : 0.f;
     int nme_arg = 0, nme = 0xf;  // next_move_to_exit (:113-118)
     if (s.f(MM_AF_KNOWS_END) && !v.is_end(s.x, s.y)) {
         nme_arg = (v.tdir(s.x, s.y) - s.dir) & 3;
         nme = 1 << nme_arg;
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) put(53 + i, (nme >> i & 1) ? 1.f : 0.f);
-    if (hi > 57) {
-        put(57, s.exit_len < 40 ? (float)((double)s.exit_len / 40.0) : 1.f);
-        put(58, s.f(MM_AF_OTHER_KNOWS) ? 1.f : 0.f);
-        put(59, s.f(MM_AF_HAS_KEY) ? 1.f : 0.f);
-        put(60, s.f(MM_AF_TEAM_KEY) ? 1.f : 0.f);
-        put(61, s.tfls < 40 ? (float)((double)s.tfls / 40.0) : 1.f);
-        put(62, (float)((double)v.t / (double)v.max_t));
-        put(63, s.tag == 2 ? 1.f : 0.f);
-        put(64, s.tag == 3 ? 1.f : 0.f);
-    }
-    if (mk) {  // --- action mask (:132-139)
-        int nb = 0, mmask = 0;
+    for (int i = 0; i < 4; i++) o[53 + i] = (nme >> i & 1) ? 1.f : 0.f;
+    o[57] = s.exit_len < 40 ? __fdiv_rn((float)s.exit_len, 40.f) : 1.f;
+    o[58] = s.f(MM_AF_OTHER_KNOWS) ? 1.f : 0.f;
+    o[59] = s.f(MM_AF_HAS_KEY) ? 1.f : 0.f;
+    o[60] = s.f(MM_AF_TEAM_KEY) ? 1.f : 0.f;
+    o[61] = s.tfls < 40 ? __fdiv_rn((float)s.tfls, 40.f) : 1.f;
+    o[62] = __fdiv_rn((float)v.t, (float)v.max_t);
+    o[63] = s.tag == 2 ? 1.f : 0.f;
+    o[64] = s.tag == 3 ? 1.f : 0.f;
+    // action mask (:132-139)
+    int nb = 0, mmask = 0;
 #pragma unroll
-        for (int d = 0; d < 4; d++) {
-            nb |= (sum_dead(sum[d]) != 4) << d;  // open neighbour (get_neighbors, relative)
-            mmask |= (sum_dead(sum[d]) == 0) << d;
-        }
-        if (s.f(MM_AF_SEES_END) || s.f(MM_AF_SEES_KEY)) mmask = nb;
-        if (r.vk) mmask = r.vk & (-r.vk);  // one-hot at np.argmax(visible_key)
-#pragma unroll
-        for (int i = 0; i < 4; i++) mk[i] = (uint8_t)(mmask >> i & 1);
-        mk[4] = (uint8_t)(r.va != 0 && s.x == v.ex && s.x == v.ey);  // (x, x) == end (Q2)
-        mk[5] = (uint8_t)(v.type(s.x, s.y) != s.tag);
+    for (int d = 0; d < 4; d++) {
+        nb |= (sum_dead(sum[d]) != 4) << d;  // open neighbour (get_neighbors, relative)
+        mmask |= (sum_dead(sum[d]) == 0) << d;
     }
+    if (s.f(MM_AF_SEES_END) || s.f(MM_AF_SEES_KEY)) mmask = nb;
+    if (r.vk) mmask = r.vk & (-r.vk);  // one-hot at np.argmax(visible_key)
+#pragma unroll
+    for (int i = 0; i < 4; i++) mk[i] = (uint8_t)(mmask >> i & 1);
+    mk[4] = (uint8_t)(r.va != 0 && s.x == v.ex && s.x == v.ey);  // (x, x) == end (Q2)
+    mk[5] = (uint8_t)(v.type(s.x, s.y) != s.tag);
     return nme_arg;
 }
 
@@ -368,7 +358,14 @@ MM_HD int observe(const View& v, Agent& s, Agent& q, bool q_registered, OutF&& o
 #pragma unroll
     for (int d = 0; d < 4; d++) sum[d] = summarize_dir(v, s.x, s.y, s.dir, d, s.tag, q.x, q.y, q_registered);
     const Vis r = replay(v, s, q, sum);
-    return emit(v, s, r, sum, out, mk);
+    float o[kObs];
+    uint8_t m[kMask];
+    const int am = build_obs(v, s, r, sum, o, m);
+#pragma unroll
+    for (int i = 0; i < kObs; i++) out(i, o[i]);
+#pragma unroll
+    for (int i = 0; i < kMask; i++) mk[i] = m[i];
+    return am;
 }
 
 // single_agent_step (maze.py:124-163).  Returns 1 if this agent picked up the

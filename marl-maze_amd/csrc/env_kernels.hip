@@ -374,7 +374,6 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     }
     copy_in(smem, env.layout + (size_t)m0 * stride, nb * stride);
     __syncthreads();
-    if (!valid) return;
     View v;
     v.L = smem + lm * stride;
     v.w = mz.w; v.h = mz.h; v.ex = mz.ex; v.ey = mz.ey; v.kx = mz.kx; v.ky = mz.ky;
@@ -382,54 +381,76 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     Agent a0 = load_agent(g0, 2);
     Agent a1 = load_agent(g1, 3);
     uint32_t status = mz.status;
-    uint8_t* gl = (q == 0) ? env.layout + (size_t)m * stride : nullptr;
-    // maze.py:75-90 (the four lanes write identical mark bytes into LDS)
-    mz.t += 1;
-    v.t = mz.t;
-    int first_key = agent_step(v, a0, ac.x, ac.y, gl, status);
-    const int have_key0 = a0.f(MM_AF_HAS_KEY);
-    first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
-    const int have_key = have_key0 + a1.f(MM_AF_HAS_KEY);
-    // geometry of this lane's two directions of agent a
-    const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
-    const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
-    const uint32_t sB = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + 1, me0.tag, ot0.x, ot0.y, true);
-    const int base = (threadIdx.x & 63) & ~3;
-    uint32_t sum0[4], sum1[4];
-    sum0[0] = __shfl(sA, base + 0);
-    sum0[1] = __shfl(sB, base + 0);
-    sum0[2] = __shfl(sA, base + 1);
-    sum0[3] = __shfl(sB, base + 1);
-    sum1[0] = __shfl(sA, base + 2);
-    sum1[1] = __shfl(sB, base + 2);
-    sum1[2] = __shfl(sA, base + 3);
-    sum1[3] = __shfl(sB, base + 3);
-    // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1
-    const Vis r0 = replay(v, a0, a1, sum0);
-    const Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
-    const bool ready0 = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
-    const Vis r1 = replay(v, a1, a0, sum1);
-    const bool exit_ready = ready0 && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
-    // this lane's half of agent a's observation row; lane h == 0 writes the mask
-    const Agent me = a ? a1 : a0_obs;
-    const Vis rm = a ? r1 : r0;
-    uint32_t sm[4];
+    float o[kObs];
+    uint8_t mk[kMask];
+    int first_key = 0, have_key = 0;
+    if (valid) {
+        uint8_t* gl = (q == 0) ? env.layout + (size_t)m * stride : nullptr;
+        // maze.py:75-90 (the four lanes write identical mark bytes into LDS)
+        mz.t += 1;
+        v.t = mz.t;
+        first_key = agent_step(v, a0, ac.x, ac.y, gl, status);
+        const int have_key0 = a0.f(MM_AF_HAS_KEY);
+        first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
+        have_key = have_key0 + a1.f(MM_AF_HAS_KEY);
+        // geometry of this lane's two directions of agent a
+        const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
+        const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
+        const uint32_t sB = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + 1, me0.tag, ot0.x, ot0.y, true);
+        const int base = (threadIdx.x & 63) & ~3;
+        uint32_t sum0[4], sum1[4];
+        sum0[0] = __shfl(sA, base + 0);
+        sum0[1] = __shfl(sB, base + 0);
+        sum0[2] = __shfl(sA, base + 1);
+        sum0[3] = __shfl(sB, base + 1);
+        sum1[0] = __shfl(sA, base + 2);
+        sum1[1] = __shfl(sB, base + 2);
+        sum1[2] = __shfl(sA, base + 3);
+        sum1[3] = __shfl(sB, base + 3);
+        // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1
+        const Vis r0 = replay(v, a0, a1, sum0);
+        const Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
+        const bool ready0 = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
+        const Vis r1 = replay(v, a1, a0, sum1);
+        const bool exit_ready = ready0 && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
+        const Agent me = a ? a1 : a0_obs;
+        const Vis rm = a ? r1 : r0;
+        uint32_t sm[4];
 #pragma unroll
-    for (int d = 0; d < 4; d++) sm[d] = a ? sum1[d] : sum0[d];
-    float* orow = obs + (size_t)(2 * m + a) * kObs;
-    uint8_t* mk = masks + (size_t)(2 * m + a) * kMask;
-    const int am = emit(v, me, rm, sm, [&](int i, float x) { orow[i] = x; }, h == 0 ? mk : nullptr,
-                        h == 0 ? 0 : 33, h == 0 ? 33 : kObs);
-    if (h == 0 && exit_ready) {  // maze.py:107-113
-        if (!v.is_end(me.x, me.y)) {
+        for (int d = 0; d < 4; d++) sm[d] = a ? sum1[d] : sum0[d];
+        const int am = build_obs(v, me, rm, sm, o, mk);
+        if (exit_ready) {  // maze.py:107-113
+            if (!v.is_end(me.x, me.y)) {
 #pragma unroll
-            for (int d = 0; d < 4; d++) mk[d] = (uint8_t)(d == am);
-        } else {
-            mk[0] = mk[1] = mk[2] = mk[3] = 0;
-            mk[4] = 1;
+                for (int d = 0; d < 4; d++) mk[d] = (uint8_t)(d == am);
+            } else {
+                mk[0] = mk[1] = mk[2] = mk[3] = 0;
+                mk[4] = 1;
+            }
         }
     }
-    if (q != 0) return;
+    // The workgroup's obs rows [2*m0, 2*(m0+nb)) and mask rows are contiguous
+    // in HBM: stage them in LDS (over the layouts, which are no longer read)
+    // and store them with 16-byte coalesced writes.
+    __syncthreads();
+    float* sobs = reinterpret_cast<float*>(smem);
+    uint8_t* smk = smem + kMPB4 * 2 * kObs * 4;
+    if (valid) {
+        float* orow = sobs + (2 * lm + a) * kObs + 33 * h;  // lane h: elements [33h, 33h + 33 - h)
+#pragma unroll
+        for (int k = 0; k < 33; k++) {
+            const float val = h ? (k < 32 ? o[33 + k] : 0.f) : o[k];
+            if (k < 32 || h == 0) orow[k] = val;
+        }
+        if (h == 0) {
+#pragma unroll
+            for (int i = 0; i < kMask; i++) smk[(2 * lm + a) * kMask + i] = mk[i];
+        }
+    }
+    __syncthreads();
+    copy_out(reinterpret_cast<uint8_t*>(obs + (size_t)2 * m0 * kObs), smem, nb * 2 * kObs * 4);
+    copy_out(masks + (size_t)2 * m0 * kMask, smk, nb * 2 * kMask);
+    if (!valid || q != 0) return;
     // reward / done (maze.py:115-121) and state write-back
     float r = first_key ? 0.5f * first_key : 0.f;
     uint8_t dn = 0;
@@ -460,7 +481,10 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     env.agents[2 * m + 1] = pack_agent(a1);
 }
 
-inline size_t step_lds_bytes(int stride) { return (size_t)((kMPB4 * stride + 15) & ~15); }
+inline size_t step_lds_bytes(int stride) {
+    const int lay = kMPB4 * stride, rows = kMPB4 * 2 * (kObs * 4 + kMask);
+    return (size_t)(((lay > rows ? lay : rows) + 15) & ~15);
+}
 
 inline int check_env(const mm_env_t* env) {
     if (!env || env->n <= 0 || !env->layout || !env->agents || !env->mazes || !env->rng || !env->work) return MM_E_ARG;
