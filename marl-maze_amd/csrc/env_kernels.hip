@@ -362,6 +362,14 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     const int a = q >> 1, h = q & 1;
     const int m = m0 + lm;
     const bool valid = lm < nb;
+#ifdef MM_STEP_STAMPS  // tools/step_stamps.py: per-workgroup phase clocks into work[64 + 8*block]
+    uint64_t st[6];
+    st[0] = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#define MM_STAMP(i) st[i] = __builtin_amdgcn_s_memtime()
+#else
+#define MM_STAMP(i)
+#endif
     // per-maze state loads are issued before the layout staging barrier
     mm_maze_t mz{};
     mm_agent_t g0{}, g1{};
@@ -374,6 +382,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     }
     copy_in(smem, env.layout + (size_t)m0 * stride, nb * stride);
     __syncthreads();
+    MM_STAMP(1);
     View v;
     v.L = smem + lm * stride;
     v.w = mz.w; v.h = mz.h; v.ex = mz.ex; v.ey = mz.ey; v.kx = mz.kx; v.ky = mz.ky;
@@ -429,6 +438,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
             }
         }
     }
+    MM_STAMP(2);
     // The workgroup's obs rows [2*m0, 2*(m0+nb)) and mask rows are contiguous
     // in HBM: stage them in LDS (over the layouts, which are no longer read)
     // and store them with 16-byte coalesced writes.
@@ -448,8 +458,18 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
         }
     }
     __syncthreads();
+    MM_STAMP(3);
     copy_out(reinterpret_cast<uint8_t*>(obs + (size_t)2 * m0 * kObs), smem, nb * 2 * kObs * 4);
     copy_out(masks + (size_t)2 * m0 * kMask, smk, nb * 2 * kMask);
+    MM_STAMP(4);
+#ifdef MM_STEP_STAMPS
+    if (threadIdx.x == 0) {
+        int32_t* w = env.work + kListOff + 8 * blockIdx.x;
+        for (int i = 1; i < 5; i++) w[i - 1] = (int32_t)(st[i] - st[0]);
+        w[4] = (int32_t)(uint32_t)rt0;
+        w[5] = (int32_t)(uint32_t)__builtin_amdgcn_s_memrealtime();
+    }
+#endif
     if (!valid || q != 0) return;
     // reward / done (maze.py:115-121) and state write-back
     float r = first_key ? 0.5f * first_key : 0.f;

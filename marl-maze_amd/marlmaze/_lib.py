@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime first: the .so binds to it)
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libmarlmaze.so")
+# MARLMAZE_LIB: an alternative build of the same library (instrumented builds under tools/)
+LIB_PATH = os.environ.get("MARLMAZE_LIB") or os.path.join(PKG_ROOT, "libmarlmaze.so")
 
 OBS_DIM = 65
 MASK_DIM = 6
