@@ -122,24 +122,27 @@ struct DirWin {
     uint32_t m3;     //                                    ... of tag 3
 };
 
-MM_HD int cell_at(const View& v, int x, int y) {  // reference cell value, 1 outside the grid
-    const int cx = min(max(x, 0), v.w - 1), cy = min(max(y, 0), v.h - 1);
-    const int c = v.L[cy * v.w + cx] & 3;
-    return v.inb(x, y) ? c : 1;
-}
-
 MM_HD DirWin gather_dir(const View& v, int x, int y, int ad) {
-    const int ar = (ad + 1) & 3, al = (ad + 3) & 3;
+    const int dx = ddx(ad), dy = ddy(ad);
+    const int sx = ddx((ad + 1) & 3), sy = ddy((ad + 1) & 3);  // right-hand side; left = -(sx, sy)
+    // in-bounds cells along the ray, and whether each side row/column exists
+    const int lim = dx > 0 ? v.w - 1 - x : (dx < 0 ? x : (dy > 0 ? v.h - 1 - y : y));
+    const bool okr = (unsigned)(x + sx) < (unsigned)v.w && (unsigned)(y + sy) < (unsigned)v.h;
+    const bool okl = (unsigned)(x - sx) < (unsigned)v.w && (unsigned)(y - sy) < (unsigned)v.h;
+    const int step = dx + dy * v.w;
+    const int offr = okr ? sx + sy * v.w : 0, offl = okl ? -(sx + sy * v.w) : 0;
+    const uint8_t* base = v.L + y * v.w + x;
     DirWin w{0, 0, 0, 0};
 #pragma unroll
     for (int j = 1; j <= 5; j++) {
-        const int cx = x + j * ddx(ad), cy = y + j * ddy(ad);
-        const int c = cell_at(v, cx, cy);
-        w.fwd |= (uint32_t)(c != 1) << (j - 1);
+        const bool in = j <= lim;
+        const uint8_t* cp = base + min(j, lim) * step;  // clamped: never leaves the maze
+        const int c = cp[0] & 3;
+        w.fwd |= (uint32_t)(in && c != 1) << (j - 1);
         if (j <= 4) {
-            w.m2 |= (uint32_t)(c == 2) << (j - 1);
-            w.m3 |= (uint32_t)(c == 3) << (j - 1);
-            const bool so = cell_at(v, cx + ddx(ar), cy + ddy(ar)) != 1 || cell_at(v, cx + ddx(al), cy + ddy(al)) != 1;
+            w.m2 |= (uint32_t)(in && c == 2) << (j - 1);
+            w.m3 |= (uint32_t)(in && c == 3) << (j - 1);
+            const bool so = in && ((okr && (cp[offr] & 3) != 1) || (okl && (cp[offl] & 3) != 1));
             w.side |= (uint32_t)so << (j - 1);
         }
     }
@@ -149,12 +152,10 @@ MM_HD DirWin gather_dir(const View& v, int x, int y, int ad) {
 // Distance j (1..L) at which the ray from (x, y) in absolute direction ad
 // passes (tx, ty); 0 if it does not within the L visible cells.
 MM_HD int ray_hit(int x, int y, int ad, int tx, int ty, int L) {
-    int j;
-    if (ad == 0) j = (tx == x) ? y - ty : 0;
-    else if (ad == 1) j = (ty == y) ? tx - x : 0;
-    else if (ad == 2) j = (tx == x) ? ty - y : 0;
-    else j = (ty == y) ? x - tx : 0;
-    return (j >= 1 && j <= L) ? j : 0;
+    const int dx = ddx(ad), dy = ddy(ad);
+    const int rx = tx - x, ry = ty - y;
+    const int j = rx * dx + ry * dy;
+    return (rx == j * dx && ry == j * dy && j >= 1 && j <= L) ? j : 0;
 }
 
 // Geometry of one relative direction d of an observation, packed in a word:
@@ -175,17 +176,12 @@ MM_HD uint32_t summarize_dir(const View& v, int x, int y, int dir, int d, int ta
     const uint32_t vis = (1u << L) - 1u;
     const int own = __builtin_popcount((tag == 2 ? w.m2 : w.m3) & vis);
     const int oth = __builtin_popcount((tag == 2 ? w.m3 : w.m2) & vis);
-    int dead = (w.fwd & 1u) ? 0 : 4;  // get_dead_ends (:150-181)
-    if (w.fwd & 1u) {
-#pragma unroll
-        for (int j = 1; j <= 4; j++) {
-            if (w.side >> (j - 1) & 1u) break;   // a turn: not a dead end
-            if (!(w.fwd >> j & 1u)) {           // only the way back is open
-                dead = 4 - j;
-                break;
-            }
-        }
-    }
+    // get_dead_ends (:150-181): walk j = 1..4 while cell j is open; a side
+    // opening ends the walk (not a dead end), a closed cell j+1 makes cell j
+    // a dead end at distance j.
+    const uint32_t stop = (w.side | ~(w.fwd >> 1)) & 0xfu;
+    const int j0 = __builtin_ctz(stop | 0x10u) + 1;  // 5: no stop within 4 cells
+    const int dead = !(w.fwd & 1u) ? 4 : ((j0 <= 4 && !(w.side >> (j0 - 1) & 1u)) ? 4 - j0 : 0);
     return (uint32_t)L | (uint32_t)je << 3 | (uint32_t)jk << 6 | (uint32_t)ja << 9 | (uint32_t)own << 12 |
            (uint32_t)oth << 15 | (uint32_t)dead << 18;
 }
@@ -198,21 +194,6 @@ MM_HD int sum_own(uint32_t s) { return s >> 12 & 7; }
 MM_HD int sum_oth(uint32_t s) { return s >> 15 & 7; }
 MM_HD int sum_dead(uint32_t s) { return s >> 18 & 7; }
 
-// The other agent seen on ray d at distance j (maze_agent.py:239-260).
-MM_HD void sight_agent(Agent& s, Agent& q, int d, int j, int& va, int& vad) {
-    s.tfls = 0;
-    s.olsx = q.x;
-    s.olsy = q.y;
-    if (q.f(MM_AF_KNOWS_END)) s.flags |= MM_AF_OTHER_KNOWS;
-    if (q.f(MM_AF_HAS_KEY)) s.flags |= MM_AF_TEAM_KEY;
-    vad |= 1 << q.dir;
-    va |= 1 << d;
-    if (j == 1 && s.f(MM_AF_KNOWS_END) && !q.f(MM_AF_KNOWS_END)) {
-        s.flags |= MM_AF_OTHER_KNOWS;  // route copy + push/pop (:253-257) == tree path
-        q.flags |= MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS;
-    }
-}
-
 struct Vis {
     int va, vk, vad;  // visible agents / key per relative ray, other agent's facing (bitmasks)
 };
@@ -221,51 +202,74 @@ struct Vis {
 // replays, from the four direction summaries, every state change the
 // reference makes -- in its order (directions 0..3, cells in increasing j, a
 // cell's end check before its agent check) -- on the observer s and on the
-// other agent q.
+// other agent q.  Written with selects: the mazes of a wavefront take
+// different paths, so branches would serialise.
 MM_HD Vis replay(const View& v, Agent& s, Agent& q, const uint32_t sum[4]) {
     Vis r{0, 0, 0};
-    s.tfls += 1;
+    int sf = s.flags, qf = q.flags;
+    int tfls = s.tfls + 1;
+    int olsx = s.olsx, olsy = s.olsy;
+    int exit_len = s.exit_len;
+    int minx = s.minx, maxx = s.maxx, miny = s.miny, maxy = s.maxy;
     bool sees_end = v.is_end(s.x, s.y);
-    bool sees_key = false;
-    if (q.x == s.x && q.y == s.y) {  // co-location (:199-213); q's state may be stale (Q3)
-        s.tfls = 0;
-        r.va = 0xf;
-        s.olsx = q.x;
-        s.olsy = q.y;
-        if (q.f(MM_AF_HAS_KEY)) s.flags |= MM_AF_TEAM_KEY;
-        if (q.f(MM_AF_KNOWS_END)) s.flags |= MM_AF_OTHER_KNOWS;
-        r.vad |= 1 << q.dir;
-        if (s.f(MM_AF_KNOWS_END) && !q.f(MM_AF_KNOWS_END)) {  // route copy (implicit: tree path)
-            s.flags |= MM_AF_OTHER_KNOWS;
-            q.flags |= MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS;
-        }
+    int vk = 0;
+    const int share = ((qf & MM_AF_HAS_KEY) ? MM_AF_TEAM_KEY : 0) | ((qf & MM_AF_KNOWS_END) ? MM_AF_OTHER_KNOWS : 0);
+    // co-location (:199-213); q's state may be stale (Q3).  The route copy
+    // (implicit: tree path) marks both as knowing.
+    const bool coloc = q.x == s.x && q.y == s.y;
+    {
+        const bool copy = coloc && (sf & MM_AF_KNOWS_END) && !(qf & MM_AF_KNOWS_END);
+        tfls = coloc ? 0 : tfls;
+        r.va = coloc ? 0xf : 0;
+        r.vad = coloc ? 1 << q.dir : 0;
+        olsx = coloc ? q.x : olsx;
+        olsy = coloc ? q.y : olsy;
+        sf |= coloc ? share : 0;
+        sf |= copy ? MM_AF_OTHER_KNOWS : 0;
+        qf |= copy ? (MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS) : 0;
     }
 #pragma unroll
     for (int d = 0; d < 4; d++) {  // rays (:215-269)
         const uint32_t sm = sum[d];
         const int L = sum_L(sm), je = sum_je(sm), jk = sum_jk(sm), ja = sum_ja(sm);
-        const bool agent_first = ja && je && ja < je;
-        if (ja && agent_first) sight_agent(s, q, d, ja, r.va, r.vad);
-        if (je) {
-            s.flags |= MM_AF_KNOWS_END;
-            sees_end = true;
-            if (s.exit_len == -1) s.exit_len = je;  // route := [ad]*j == tree path
-        }
-        if (jk) {
-            sees_key = true;
-            r.vk |= 1 << d;
-        }
-        if (ja && !agent_first) sight_agent(s, q, d, ja, r.va, r.vad);
-        if (L) {  // update_maze_minmax (:313-328): the farthest visible cell decides
-            const int ad = (d + s.dir) & 3;
-            if (ad == 0) s.miny = min(s.miny, s.y - L);
-            else if (ad == 1) s.maxx = max(s.maxx, s.x + L);
-            else if (ad == 2) s.maxy = max(s.maxy, s.y + L);
-            else s.minx = min(s.minx, s.x - L);
-        }
+        // the other agent on this ray (:239-260); when it stands beyond the
+        // end cell, the end check of this ray runs first
+        const int known = (sf | ((je && !(ja && ja < je)) ? MM_AF_KNOWS_END : 0)) & MM_AF_KNOWS_END;
+        const int shr = ((qf & MM_AF_HAS_KEY) ? MM_AF_TEAM_KEY : 0) | ((qf & MM_AF_KNOWS_END) ? MM_AF_OTHER_KNOWS : 0);
+        const bool copy = ja == 1 && known && !(qf & MM_AF_KNOWS_END);
+        tfls = ja ? 0 : tfls;
+        olsx = ja ? q.x : olsx;
+        olsy = ja ? q.y : olsy;
+        sf |= ja ? shr : 0;
+        r.vad |= ja ? 1 << q.dir : 0;
+        r.va |= ja ? 1 << d : 0;
+        sf |= copy ? MM_AF_OTHER_KNOWS : 0;
+        qf |= copy ? (MM_AF_KNOWS_END | MM_AF_OTHER_KNOWS) : 0;
+        // the end on this ray
+        sf |= je ? MM_AF_KNOWS_END : 0;
+        sees_end = sees_end || je;
+        exit_len = (je && exit_len == -1) ? je : exit_len;  // route := [ad]*j == tree path
+        vk |= jk ? 1 << d : 0;
+        // update_maze_minmax (:313-328): the farthest visible cell decides
+        const int ad = (d + s.dir) & 3;
+        miny = (L && ad == 0) ? min(miny, s.y - L) : miny;
+        maxx = (L && ad == 1) ? max(maxx, s.x + L) : maxx;
+        maxy = (L && ad == 2) ? max(maxy, s.y + L) : maxy;
+        minx = (L && ad == 3) ? min(minx, s.x - L) : minx;
     }
-    s.set(MM_AF_SEES_END, sees_end);
-    s.set(MM_AF_SEES_KEY, sees_key);
+    sf = sees_end ? (sf | MM_AF_SEES_END) : (sf & ~MM_AF_SEES_END);
+    sf = vk ? (sf | MM_AF_SEES_KEY) : (sf & ~MM_AF_SEES_KEY);
+    s.flags = sf;
+    q.flags = qf;
+    s.tfls = tfls;
+    s.olsx = olsx;
+    s.olsy = olsy;
+    s.exit_len = exit_len;
+    s.minx = minx;
+    s.maxx = maxx;
+    s.miny = miny;
+    s.maxy = maxy;
+    r.vk = vk;
     return r;
 }
 

@@ -362,8 +362,8 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     const int a = q >> 1, h = q & 1;
     const int m = m0 + lm;
     const bool valid = lm < nb;
-#ifdef MM_STEP_STAMPS  // tools/step_stamps.py: per-workgroup phase clocks into work[64 + 8*block]
-    uint64_t st[6];
+#ifdef MM_STEP_STAMPS  // tools/step_stamps.py: per-workgroup phase clocks into work[64 + 12*block]
+    uint64_t st[10];
     st[0] = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #define MM_STAMP(i) st[i] = __builtin_amdgcn_s_memtime()
@@ -402,6 +402,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
         const int have_key0 = a0.f(MM_AF_HAS_KEY);
         first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
         have_key = have_key0 + a1.f(MM_AF_HAS_KEY);
+        MM_STAMP(5);
         // geometry of this lane's two directions of agent a
         const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
         const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
@@ -416,12 +417,14 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
         sum1[1] = __shfl(sB, base + 2);
         sum1[2] = __shfl(sA, base + 3);
         sum1[3] = __shfl(sB, base + 3);
+        MM_STAMP(6);
         // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1
         const Vis r0 = replay(v, a0, a1, sum0);
         const Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
         const bool ready0 = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
         const Vis r1 = replay(v, a1, a0, sum1);
         const bool exit_ready = ready0 && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
+        MM_STAMP(7);
         const Agent me = a ? a1 : a0_obs;
         const Vis rm = a ? r1 : r0;
         uint32_t sm[4];
@@ -464,10 +467,13 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     MM_STAMP(4);
 #ifdef MM_STEP_STAMPS
     if (threadIdx.x == 0) {
-        int32_t* w = env.work + kListOff + 8 * blockIdx.x;
+        int32_t* w = env.work + kListOff + 12 * blockIdx.x;
         for (int i = 1; i < 5; i++) w[i - 1] = (int32_t)(st[i] - st[0]);
         w[4] = (int32_t)(uint32_t)rt0;
         w[5] = (int32_t)(uint32_t)__builtin_amdgcn_s_memrealtime();
+        w[6] = (int32_t)(st[5] - st[0]);
+        w[7] = (int32_t)(st[6] - st[5]);  // summaries
+        w[8] = (int32_t)(st[7] - st[6]);  // replays
     }
 #endif
     if (!valid || q != 0) return;

@@ -54,8 +54,9 @@ for i in range(a.steps):
         env.reset(env.done, obs=obs, masks=masks)
 torch.cuda.synchronize()
 grid = (n + 31) // 32
-w = env.work[64:64 + 8 * grid].view(grid, 8).cpu().numpy().astype(np.int64)
+w = env.work[64:64 + 12 * grid].view(grid, 12).cpu().numpy().astype(np.int64)
 ph = w[:, :4]
+st5 = w[:, 6]
 rt0 = w[:, 4] & 0xffffffff
 rt1 = w[:, 5] & 0xffffffff
 base = rt0.min()
@@ -70,6 +71,8 @@ def q(x):
 print(json.dumps({
     "blocks": grid,
     "cycles_load": q(ph[:, 0]), "cycles_compute": q(ph[:, 1] - ph[:, 0]),
+    "cycles_agent_step": q(st5 - ph[:, 0]), "cycles_summaries": q(w[:, 7]), "cycles_replays": q(w[:, 8]),
+    "cycles_build_obs": q(ph[:, 1] - (st5 + w[:, 7] + w[:, 8])),
     "cycles_stage": q(ph[:, 2] - ph[:, 1]), "cycles_store": q(ph[:, 3] - ph[:, 2]),
     "cycles_total": q(ph[:, 3]),
     "block_us": q(end_us - start_us), "start_us": q(start_us), "end_us": q(end_us),
