@@ -34,6 +34,7 @@ import torch
 
 from . import ops
 from .dist import DP
+from .gemm_tuning import enable_tuned_gemms
 from .networks import Actor, Critic
 from .vecmaze import VecMaze
 
@@ -44,12 +45,14 @@ class PPO:
     def __init__(self, agent_amount, epochs=500, batch_size=15000, lr=0.0002, discount_rate=0.99, lam=0.95,
                  updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
                  seed=3234, sample_seed=None, device=None, model_path=MODEL_PATH, load=True, parity_mode=True,
-                 bootstrap=True, dp=None, verbose=True, save=True):
+                 bootstrap=True, dp=None, verbose=True, save=True, tuned_gemms=True):
         self.maze = None  # wired by Maze.__init__ (maze.py:39-42), as in the reference
         self.dp = dp if dp is not None else DP.single()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
+        if tuned_gemms and self.device.type == "cuda":  # pre-tuned library GEMM choice (gemm_tuning.py)
+            enable_tuned_gemms()
         # networks are built on the CPU right after the seed, like PPO.py:7,16-17
         g = torch.random.get_rng_state()
         torch.manual_seed(seed)
