@@ -16,7 +16,8 @@
 // Backward: persistent grid; each workgroup accumulates the weight gradients
 //           of the rows it owns in registers (fixed entry -> thread map, so the
 //           sum order is deterministic) and writes ONE partial row of
-//           kGradLen floats; the caller sums the partial rows.
+//           kGradLen floats; the caller sums the partial rows.  Sized for two
+//           256-thread workgroups per CU (grid = 2 x CUs).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -205,38 +206,33 @@ __global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __rest
 // ---------------------------------------------------------------------------
 // backward (persistent, in-kernel weight-gradient reduction)
 // ---------------------------------------------------------------------------
-constexpr int kBwdRows = 4;      // samples per iteration of a 128-thread workgroup
-constexpr int kBwdThreads = 128;
+// 256 threads = 8 samples per iteration (32-lane group g = sample, lane i =
+// token).  LDS per sample (floats): attention phase {K 23x10 | Q 23x10 |
+// V 23x20 | P 23x23 | dS 23x23}; after a barrier the same words hold the
+// weight-gradient operands {G = [dq|dk|dv] 23x40 | T 23x20 | dT 23x20 | X 23x4}.
+// dctx rows are re-read from global (L1/L2) rather than staged.  With the
+// Q/K/V weights that is 66.5 KB per workgroup: two workgroups (8 waves) per CU.
+constexpr int kBwdRows = 8;
+constexpr int kBwdThreads = 256;
+constexpr int kOffK = 0, kOffQ = 230, kOffV = 460, kOffP = 920, kOffS = 1449;  // attention phase
+constexpr int kOffG = 0, kOffT = 920, kOffD = 1380, kOffX = 1840;               // weight-gradient phase
+constexpr int kSampleF = 1980;  // floats per sample (>= 1978 and >= 1932; multiple of 4)
 constexpr int kQkvQuads = (2 * kKq + kEmb) * (kEmb / 4);  // 200 (row a, columns 4b..4b+3) of [40 x 20]
 constexpr int kPQuads = kTok * kEmb;                      // 460 (token i, channel c) x 4 inputs
-constexpr int kQ1 = (kQkvQuads + kBwdThreads - 1) / kBwdThreads;  // 2
-constexpr int kP1 = (kPQuads + kBwdThreads - 1) / kBwdThreads;    // 4
+constexpr int kP1 = (kPQuads + kBwdThreads - 1) / kBwdThreads;  // 2
 
-struct BwdLds {
-    float Q[kBwdRows][kTok][kKq];
-    float K[kBwdRows][kTok][kKq];
-    float V[kBwdRows][kTok][kEmb];
-    float T[kBwdRows][kTok][kEmb];
-    float C[kBwdRows][kTok][kEmb];     // dctx = dh
-    float P[kBwdRows][kTok][kTok + 1];
-    float S[kBwdRows][kTok][kTok + 1];  // dS
-    float G[kBwdRows][kTok][2 * kKq + kEmb];  // [dq | dk | dv] per token
-    float D[kBwdRows][kTok][kEmb];     // dt
-    float X[kBwdRows][kTok][kPin];     // token input slices
-};
-
-__global__ __launch_bounds__(kBwdThreads) void k_front_bwd(FrontW W, const float* __restrict__ x, int ldx, int B,
-                                                           int parity, const float* __restrict__ dh,
-                                                           float* __restrict__ partial) {
-    __shared__ __attribute__((aligned(16))) BwdLds L;
+__global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const float* __restrict__ x, int ldx, int B,
+                                                              int parity, const float* __restrict__ dh,
+                                                              float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kSampleF];
     __shared__ __attribute__((aligned(16))) WLds Ws;
     stage_w(W, Ws);
     const int g = threadIdx.x >> 5;
     const int i = threadIdx.x & 31;
-    // weight-gradient accumulators owned by this thread
-    float aq[kQ1][4], ap[kP1][4], ab[kP1];
-#pragma unroll
-    for (int u = 0; u < kQ1; u++) aq[u][0] = aq[u][1] = aq[u][2] = aq[u][3] = 0.f;
+    float* my = sm + g * kSampleF;
+    // weight-gradient accumulators owned by this thread (fixed entry map)
+    float aq[4] = {0.f, 0.f, 0.f, 0.f};
+    float ap[kP1][4], ab[kP1];
 #pragma unroll
     for (int u = 0; u < kP1; u++) {
         ap[u][0] = ap[u][1] = ap[u][2] = ap[u][3] = 0.f;
@@ -244,54 +240,53 @@ __global__ __launch_bounds__(kBwdThreads) void k_front_bwd(FrontW W, const float
     }
     const int iters = (B + kBwdRows - 1) / kBwdRows;
     for (int it = blockIdx.x; it < iters; it += gridDim.x) {
-        const int row = it * kBwdRows + g;
-        const bool act = (i < kTok) && (row < B);
-        __syncthreads();  // previous iteration's readers are done with L
-        float t[kEmb], q[kKq], dctx[kEmb];
-        if (i < kTok) {
-            if (act) {
-                const float4 xv = xslice(x + (size_t)row * ldx, i, parity != 0);
-                *reinterpret_cast<float4*>(L.X[g][i]) = xv;
-                embed(W, xv, i, t);
-                float k[kKq], v[kEmb];
-                matvec<kKq>(Ws, 0, t, q);
-                matvec<kKq>(Ws, kKq, t, k);
-                matvec<kEmb>(Ws, 2 * kKq, t, v);
-                const float* dhi = dh + (size_t)row * kRowF + i * kEmb;
+        const int row0 = it * kBwdRows;
+        const int nrow = min(kBwdRows, B - row0);
+        const int row = row0 + g;
+        const bool act = (i < kTok) && (g < nrow);
+        __syncthreads();  // Ws staged / previous iteration's weight-gradient readers done
+        float dctx[kEmb];
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float* dhr = dh + (size_t)row * kRowF;
+        if (act) {  // phase 1: embedding, q/k/v
+            xv = xslice(x + (size_t)row * ldx, i, parity != 0);
+            float t[kEmb], q[kKq], k[kKq], v[kEmb];
+            embed(W, xv, i, t);
+            matvec<kKq>(Ws, 0, t, q);
+            matvec<kKq>(Ws, kKq, t, k);
+            matvec<kEmb>(Ws, 2 * kKq, t, v);
 #pragma unroll
-                for (int c = 0; c < kEmb; c += 4) {
-                    const float4 d4 = *reinterpret_cast<const float4*>(dhi + c);
-                    dctx[c] = d4.x;
-                    dctx[c + 1] = d4.y;
-                    dctx[c + 2] = d4.z;
-                    dctx[c + 3] = d4.w;
-                }
-#pragma unroll
-                for (int a = 0; a < kKq; a++) {
-                    L.Q[g][i][a] = q[a];
-                    L.K[g][i][a] = k[a];
-                }
-#pragma unroll
-                for (int c = 0; c < kEmb; c++) {
-                    L.V[g][i][c] = v[c];
-                    L.T[g][i][c] = t[c];
-                    L.C[g][i][c] = dctx[c];
-                }
-            } else {  // padding rows contribute nothing to the weight gradients
-                *reinterpret_cast<float4*>(L.X[g][i]) = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int a = 0; a < kKq; a++) L.Q[g][i][a] = L.K[g][i][a] = 0.f;
-#pragma unroll
-                for (int c = 0; c < kEmb; c++) L.V[g][i][c] = L.T[g][i][c] = L.C[g][i][c] = 0.f;
+            for (int c = 0; c < kEmb; c += 4) {
+                const float4 d4 = *reinterpret_cast<const float4*>(dhr + i * kEmb + c);
+                dctx[c] = d4.x;
+                dctx[c + 1] = d4.y;
+                dctx[c + 2] = d4.z;
+                dctx[c + 3] = d4.w;
             }
+#pragma unroll
+            for (int a = 0; a < kKq; a += 2) {
+                *reinterpret_cast<float2*>(my + kOffK + i * kKq + a) = make_float2(k[a], k[a + 1]);
+                *reinterpret_cast<float2*>(my + kOffQ + i * kKq + a) = make_float2(q[a], q[a + 1]);
+            }
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4)
+                *reinterpret_cast<float4*>(my + kOffV + i * kEmb + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
         }
         __syncthreads();
-        if (act) {
+        float dq[kKq];
+        if (act) {  // phase 2: softmax row i, dP, dS, dq
+            float q[kKq];
+#pragma unroll
+            for (int a = 0; a < kKq; a += 2) {
+                const float2 q2 = *reinterpret_cast<const float2*>(my + kOffQ + i * kKq + a);
+                q[a] = q2.x;
+                q[a + 1] = q2.y;
+            }
             float p[kTok];
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                p[j] = dot4<kKq>(q, L.K[g][j]) / kSqrtKq;
+                p[j] = dot4<kKq>(q, my + kOffK + j * kKq) / kSqrtKq;
                 mx = fmaxf(mx, p[j]);
             }
             float sum = 0.f;
@@ -305,73 +300,83 @@ __global__ __launch_bounds__(kBwdThreads) void k_front_bwd(FrontW W, const float
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
                 p[j] = p[j] / sum;
-                dp[j] = dot4<kEmb>(dctx, L.V[g][j]);  // dP_ij = dctx_i . v_j
+                dp[j] = dot4<kEmb>(dctx, my + kOffV + j * kEmb);  // dP_ij = dctx_i . v_j
                 rs = fmaf(dp[j], p[j], rs);
             }
-            float dq[kKq];
 #pragma unroll
             for (int a = 0; a < kKq; a++) dq[a] = 0.f;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
                 const float ds = (p[j] * (dp[j] - rs)) / kSqrtKq;  // softmax backward, then / sqrt(10)
-                L.P[g][i][j] = p[j];
-                L.S[g][i][j] = ds;
-                axpy4<kKq>(dq, ds, L.K[g][j]);
+                my[kOffP + i * kTok + j] = p[j];
+                my[kOffS + i * kTok + j] = ds;
+                axpy4<kKq>(dq, ds, my + kOffK + j * kKq);
             }
-#pragma unroll
-            for (int a = 0; a < kKq; a++) L.G[g][i][a] = dq[a];
-        } else if (i < kTok) {
-#pragma unroll
-            for (int j = 0; j < kTok; j++) L.P[g][i][j] = L.S[g][i][j] = 0.f;
-#pragma unroll
-            for (int a = 0; a < kKq; a++) L.G[g][i][a] = 0.f;
         }
         __syncthreads();
-        if (i < kTok) {
-            // dv_i = sum_j P_ji dctx_j ; dk_i = sum_j dS_ji q_j
-            float dv[kEmb], dk[kKq];
+        float dk[kKq], dv[kEmb], dt[kEmb], t[kEmb];
+        if (act) {  // phase 3: dv_i = sum_j P_ji dctx_j, dk_i = sum_j dS_ji q_j, dt_i
 #pragma unroll
             for (int c = 0; c < kEmb; c++) dv[c] = 0.f;
 #pragma unroll
             for (int a = 0; a < kKq; a++) dk[a] = 0.f;
-#pragma unroll
+#pragma unroll 4
             for (int j = 0; j < kTok; j++) {
-                axpy4<kEmb>(dv, L.P[g][j][i], L.C[g][j]);
-                axpy4<kKq>(dk, L.S[g][j][i], L.Q[g][j]);
+                const float pj = my[kOffP + j * kTok + i];
+                const float sj = my[kOffS + j * kTok + i];
+                const float4* cj = reinterpret_cast<const float4*>(dhr + j * kEmb);
+#pragma unroll
+                for (int c = 0; c < kEmb / 4; c++) {
+                    const float4 v = cj[c];
+                    dv[4 * c] = fmaf(pj, v.x, dv[4 * c]);
+                    dv[4 * c + 1] = fmaf(pj, v.y, dv[4 * c + 1]);
+                    dv[4 * c + 2] = fmaf(pj, v.z, dv[4 * c + 2]);
+                    dv[4 * c + 3] = fmaf(pj, v.w, dv[4 * c + 3]);
+                }
+                axpy4<kKq>(dk, sj, my + kOffQ + j * kKq);
             }
-#pragma unroll
-            for (int a = 0; a < kKq; a++) L.G[g][i][kKq + a] = dk[a];
-#pragma unroll
-            for (int c = 0; c < kEmb; c++) L.G[g][i][2 * kKq + c] = dv[c];
             // dt_i = dctx_i (residual) + Wq^T dq + Wk^T dk + Wv^T dv
-            float dt[kEmb];
 #pragma unroll
-            for (int b = 0; b < kEmb; b++) dt[b] = L.C[g][i][b];
+            for (int b = 0; b < kEmb; b++) dt[b] = dctx[b];
 #pragma unroll
             for (int r = 0; r < 2 * kKq + kEmb; r++) {
-                const float gr = (r < kKq) ? L.G[g][i][r] : (r < 2 * kKq ? dk[r - kKq] : dv[r - 2 * kKq]);
+                const float gr = (r < kKq) ? dq[r] : (r < 2 * kKq ? dk[r - kKq] : dv[r - 2 * kKq]);
                 axpy4<kEmb>(dt, gr, Ws.w[r]);
             }
+        }
+        __syncthreads();  // attention-phase words are dead: reuse them for the gradient operands
+        if (act) {
+            embed(W, xv, i, t);  // recomputed rather than held in registers through phases 2-3
+            float* G = my + kOffG + i * (2 * kKq + kEmb);
 #pragma unroll
-            for (int c = 0; c < kEmb; c++) L.D[g][i][c] = dt[c];
+            for (int a = 0; a < kKq; a += 2) {
+                *reinterpret_cast<float2*>(G + a) = make_float2(dq[a], dq[a + 1]);
+                *reinterpret_cast<float2*>(G + kKq + a) = make_float2(dk[a], dk[a + 1]);
+            }
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4) {
+                *reinterpret_cast<float4*>(G + 2 * kKq + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+                *reinterpret_cast<float4*>(my + kOffT + i * kEmb + c) = make_float4(t[c], t[c + 1], t[c + 2], t[c + 3]);
+                *reinterpret_cast<float4*>(my + kOffD + i * kEmb + c) =
+                    make_float4(dt[c], dt[c + 1], dt[c + 2], dt[c + 3]);
+            }
+            *reinterpret_cast<float4*>(my + kOffX + i * kPin) = xv;
         }
         __syncthreads();
-        // weight gradients of this iteration's rows, fixed thread -> entry map
+        // phase 4: weight gradients of this iteration's nrow samples
+        if (threadIdx.x < kQkvQuads) {
+            const int r = threadIdx.x / (kEmb / 4), c4 = threadIdx.x % (kEmb / 4);
+            for (int gg = 0; gg < nrow; gg++) {
+                const float* sg = sm + gg * kSampleF;
 #pragma unroll
-        for (int u = 0; u < kQ1; u++) {
-            const int e = threadIdx.x + u * kBwdThreads;  // quad over [40 x 20]
-            if (e < kQkvQuads) {
-                const int r = e / (kEmb / 4), c4 = e % (kEmb / 4);
-                for (int gg = 0; gg < kBwdRows; gg++)
-#pragma unroll
-                    for (int j = 0; j < kTok; j++) {
-                        const float gr = L.G[gg][j][r];
-                        const float4 tv = reinterpret_cast<const float4*>(L.T[gg][j])[c4];
-                        aq[u][0] = fmaf(gr, tv.x, aq[u][0]);
-                        aq[u][1] = fmaf(gr, tv.y, aq[u][1]);
-                        aq[u][2] = fmaf(gr, tv.z, aq[u][2]);
-                        aq[u][3] = fmaf(gr, tv.w, aq[u][3]);
-                    }
+                for (int j = 0; j < kTok; j++) {
+                    const float gr = sg[kOffG + j * (2 * kKq + kEmb) + r];
+                    const float4 tv = reinterpret_cast<const float4*>(sg + kOffT + j * kEmb)[c4];
+                    aq[0] = fmaf(gr, tv.x, aq[0]);
+                    aq[1] = fmaf(gr, tv.y, aq[1]);
+                    aq[2] = fmaf(gr, tv.z, aq[2]);
+                    aq[3] = fmaf(gr, tv.w, aq[3]);
+                }
             }
         }
 #pragma unroll
@@ -379,28 +384,23 @@ __global__ __launch_bounds__(kBwdThreads) void k_front_bwd(FrontW W, const float
             const int e = threadIdx.x + u * kBwdThreads;  // (token, channel)
             if (e < kPQuads) {
                 const int tk = e / kEmb, c = e % kEmb;
-#pragma unroll
-                for (int gg = 0; gg < kBwdRows; gg++) {
-                    const float d = L.D[gg][tk][c];
-                    const float4 xv = *reinterpret_cast<const float4*>(L.X[gg][tk]);
-                    ap[u][0] = fmaf(d, xv.x, ap[u][0]);
-                    ap[u][1] = fmaf(d, xv.y, ap[u][1]);
-                    ap[u][2] = fmaf(d, xv.z, ap[u][2]);
-                    ap[u][3] = fmaf(d, xv.w, ap[u][3]);
+                for (int gg = 0; gg < nrow; gg++) {
+                    const float* sg = sm + gg * kSampleF;
+                    const float d = sg[kOffD + tk * kEmb + c];
+                    const float4 xq = *reinterpret_cast<const float4*>(sg + kOffX + tk * kPin);
+                    ap[u][0] = fmaf(d, xq.x, ap[u][0]);
+                    ap[u][1] = fmaf(d, xq.y, ap[u][1]);
+                    ap[u][2] = fmaf(d, xq.z, ap[u][2]);
+                    ap[u][3] = fmaf(d, xq.w, ap[u][3]);
                     ab[u] += d;
                 }
             }
         }
     }
     float* out = partial + (size_t)blockIdx.x * kGradLen;
-#pragma unroll
-    for (int u = 0; u < kQ1; u++) {
-        const int e = threadIdx.x + u * kBwdThreads;
-        if (e < kQkvQuads) {
-            const int r = e / (kEmb / 4), c4 = e % (kEmb / 4);
-            *reinterpret_cast<float4*>(out + kGQ + r * kEmb + 4 * c4) =
-                make_float4(aq[u][0], aq[u][1], aq[u][2], aq[u][3]);
-        }
+    if (threadIdx.x < kQkvQuads) {
+        const int r = threadIdx.x / (kEmb / 4), c4 = threadIdx.x % (kEmb / 4);
+        *reinterpret_cast<float4*>(out + kGQ + r * kEmb + 4 * c4) = make_float4(aq[0], aq[1], aq[2], aq[3]);
     }
 #pragma unroll
     for (int u = 0; u < kP1; u++) {

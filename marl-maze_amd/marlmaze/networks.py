@@ -74,6 +74,15 @@ class m_Attention(nn.Module):
         return (t + ctx).reshape(B, FEATURE_AMOUNT * EMBEDDING_DIM)
 
 
+_CUS = {}
+
+
+def _cu_count(dev):
+    if dev not in _CUS:
+        _CUS[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _CUS[dev]
+
+
 class _FusedFront(torch.autograd.Function):
     """Projection + attention + residual as one HIP kernel each way (csrc/actor_front.hip).
 
@@ -106,7 +115,7 @@ class _FusedFront(torch.autograd.Function):
         dh = dh.contiguous()
         L = _lib.lib()
         glen = L.mm_actor_front_grad_len()
-        grid = max(1, min(1024, (B + 3) // 4))
+        grid = max(1, min(2 * _cu_count(x.device), (B + 7) // 8))  # two 8-sample workgroups per CU
         partial = torch.empty((grid, glen), dtype=torch.float32, device=x.device)
         _lib.check(L.mm_actor_front_bwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
                                         int(ctx.parity), _lib.ptr(dh), _lib.ptr(partial), grid, _lib.stream_ptr()),
