@@ -81,6 +81,25 @@ __device__ __forceinline__ void embed(const FrontW& W, float4 xv, int i, float t
     }
 }
 
+// Weights read by every lane alike go through the scalar cache: a pointer in
+// the constant address space makes the uniform loads s_load_dword* into SGPRs
+// that the FMAs take as their scalar operand (no LDS traffic, no VGPRs).
+typedef const __attribute__((address_space(4))) float cfloat;
+__device__ __forceinline__ cfloat* as_const(const float* p) { return (cfloat*)p; }
+
+// o[a] = sum_b w[a][b] t[b], w = [OUT][20] row-major in global memory (scalar loads)
+template <int OUT>
+__device__ __forceinline__ void matvec_s(const float* w, const float t[kEmb], float o[OUT]) {
+    cfloat* ws = as_const(w);
+#pragma unroll
+    for (int a = 0; a < OUT; a++) {
+        float acc = 0.f;
+#pragma unroll
+        for (int b = 0; b < kEmb; b++) acc = fmaf(ws[a * kEmb + b], t[b], acc);
+        o[a] = acc;
+    }
+}
+
 // o[a] = sum_b w[r0 + a][b] t[b]
 template <int OUT>
 __device__ __forceinline__ void matvec(const WLds& s, int r0, const float t[kEmb], float o[OUT]) {
@@ -225,26 +244,28 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
                                                               int parity, const float* __restrict__ dh,
                                                               float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kSampleF];
-    __shared__ __attribute__((aligned(16))) WLds Ws;
-    stage_w(W, Ws);
     const int g = threadIdx.x >> 5;
     const int i = threadIdx.x & 31;
     float* my = sm + g * kSampleF;
-    // weight-gradient accumulators owned by this thread (fixed entry map)
-    float aq[4] = {0.f, 0.f, 0.f, 0.f};
-    float ap[kP1][4], ab[kP1];
+    // weight-gradient accumulators, fixed entry map (deterministic sums):
+    //   dW_qkv [40 x 20] as 50 4x4 tiles x 5 token classes (j mod 5): thread t < 250
+    //   dW_p / db_p: (token, 4 channels) units: thread t < 115
+    const int qt = threadIdx.x / 5, qc = threadIdx.x % 5;  // tile (rows 4*(qt/5).., cols 4*(qt%5)..), token class
+    const int qr0 = 4 * (qt / 5), qc0 = 4 * (qt % 5);
+    float aq[4][4];
 #pragma unroll
-    for (int u = 0; u < kP1; u++) {
-        ap[u][0] = ap[u][1] = ap[u][2] = ap[u][3] = 0.f;
-        ab[u] = 0.f;
-    }
+    for (int a = 0; a < 4; a++) aq[a][0] = aq[a][1] = aq[a][2] = aq[a][3] = 0.f;
+    const int ptk = threadIdx.x / 5, pc0 = 4 * (threadIdx.x % 5);  // token, first channel
+    float ap[4][4], ab[4];
+#pragma unroll
+    for (int a = 0; a < 4; a++) ap[a][0] = ap[a][1] = ap[a][2] = ap[a][3] = ab[a] = 0.f;
     const int iters = (B + kBwdRows - 1) / kBwdRows;
     for (int it = blockIdx.x; it < iters; it += gridDim.x) {
         const int row0 = it * kBwdRows;
         const int nrow = min(kBwdRows, B - row0);
         const int row = row0 + g;
         const bool act = (i < kTok) && (g < nrow);
-        __syncthreads();  // Ws staged / previous iteration's weight-gradient readers done
+        __syncthreads();  // previous iteration's weight-gradient readers are done
         float dctx[kEmb];
         float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
         const float* dhr = dh + (size_t)row * kRowF;
@@ -252,9 +273,9 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
             xv = xslice(x + (size_t)row * ldx, i, parity != 0);
             float t[kEmb], q[kKq], k[kKq], v[kEmb];
             embed(W, xv, i, t);
-            matvec<kKq>(Ws, 0, t, q);
-            matvec<kKq>(Ws, kKq, t, k);
-            matvec<kEmb>(Ws, 2 * kKq, t, v);
+            matvec_s<kKq>(W.wq, t, q);
+            matvec_s<kKq>(W.wk, t, k);
+            matvec_s<kEmb>(W.wv, t, v);
 #pragma unroll
             for (int c = 0; c < kEmb; c += 4) {
                 const float4 d4 = *reinterpret_cast<const float4*>(dhr + i * kEmb + c);
@@ -335,14 +356,24 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
                 }
                 axpy4<kKq>(dk, sj, my + kOffQ + j * kKq);
             }
-            // dt_i = dctx_i (residual) + Wq^T dq + Wk^T dk + Wv^T dv
+            // dt_i = dctx_i (residual) + Wq^T dq + Wk^T dk + Wv^T dv (scalar-loaded weights)
+            cfloat* wq = as_const(W.wq);
+            cfloat* wk = as_const(W.wk);
+            cfloat* wv = as_const(W.wv);
 #pragma unroll
             for (int b = 0; b < kEmb; b++) dt[b] = dctx[b];
 #pragma unroll
-            for (int r = 0; r < 2 * kKq + kEmb; r++) {
-                const float gr = (r < kKq) ? dq[r] : (r < 2 * kKq ? dk[r - kKq] : dv[r - 2 * kKq]);
-                axpy4<kEmb>(dt, gr, Ws.w[r]);
-            }
+            for (int r = 0; r < kKq; r++)
+#pragma unroll
+                for (int b = 0; b < kEmb; b++) dt[b] = fmaf(dq[r], wq[r * kEmb + b], dt[b]);
+#pragma unroll
+            for (int r = 0; r < kKq; r++)
+#pragma unroll
+                for (int b = 0; b < kEmb; b++) dt[b] = fmaf(dk[r], wk[r * kEmb + b], dt[b]);
+#pragma unroll
+            for (int r = 0; r < kEmb; r++)
+#pragma unroll
+                for (int b = 0; b < kEmb; b++) dt[b] = fmaf(dv[r], wv[r * kEmb + b], dt[b]);
         }
         __syncthreads();  // attention-phase words are dead: reuse them for the gradient operands
         if (act) {
@@ -363,51 +394,66 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
             *reinterpret_cast<float4*>(my + kOffX + i * kPin) = xv;
         }
         __syncthreads();
-        // phase 4: weight gradients of this iteration's nrow samples
-        if (threadIdx.x < kQkvQuads) {
-            const int r = threadIdx.x / (kEmb / 4), c4 = threadIdx.x % (kEmb / 4);
+        // phase 4: weight gradients of this iteration's nrow samples (4x4 register tiles)
+        if (threadIdx.x < 250) {
             for (int gg = 0; gg < nrow; gg++) {
                 const float* sg = sm + gg * kSampleF;
+                for (int j = qc; j < kTok; j += 5) {
+                    const float4 gv = *reinterpret_cast<const float4*>(sg + kOffG + j * (2 * kKq + kEmb) + qr0);
+                    const float4 tv = *reinterpret_cast<const float4*>(sg + kOffT + j * kEmb + qc0);
+                    const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
-                for (int j = 0; j < kTok; j++) {
-                    const float gr = sg[kOffG + j * (2 * kKq + kEmb) + r];
-                    const float4 tv = reinterpret_cast<const float4*>(sg + kOffT + j * kEmb)[c4];
-                    aq[0] = fmaf(gr, tv.x, aq[0]);
-                    aq[1] = fmaf(gr, tv.y, aq[1]);
-                    aq[2] = fmaf(gr, tv.z, aq[2]);
-                    aq[3] = fmaf(gr, tv.w, aq[3]);
+                    for (int a = 0; a < 4; a++) {
+                        aq[a][0] = fmaf(gr[a], tv.x, aq[a][0]);
+                        aq[a][1] = fmaf(gr[a], tv.y, aq[a][1]);
+                        aq[a][2] = fmaf(gr[a], tv.z, aq[a][2]);
+                        aq[a][3] = fmaf(gr[a], tv.w, aq[a][3]);
+                    }
                 }
             }
         }
+        if (threadIdx.x < kTok * (kEmb / 4)) {
+            for (int gg = 0; gg < nrow; gg++) {
+                const float* sg = sm + gg * kSampleF;
+                const float4 dv4 = *reinterpret_cast<const float4*>(sg + kOffD + ptk * kEmb + pc0);
+                const float4 xq = *reinterpret_cast<const float4*>(sg + kOffX + ptk * kPin);
+                const float d[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
 #pragma unroll
-        for (int u = 0; u < kP1; u++) {
-            const int e = threadIdx.x + u * kBwdThreads;  // (token, channel)
-            if (e < kPQuads) {
-                const int tk = e / kEmb, c = e % kEmb;
-                for (int gg = 0; gg < nrow; gg++) {
-                    const float* sg = sm + gg * kSampleF;
-                    const float d = sg[kOffD + tk * kEmb + c];
-                    const float4 xq = *reinterpret_cast<const float4*>(sg + kOffX + tk * kPin);
-                    ap[u][0] = fmaf(d, xq.x, ap[u][0]);
-                    ap[u][1] = fmaf(d, xq.y, ap[u][1]);
-                    ap[u][2] = fmaf(d, xq.z, ap[u][2]);
-                    ap[u][3] = fmaf(d, xq.w, ap[u][3]);
-                    ab[u] += d;
+                for (int a = 0; a < 4; a++) {
+                    ap[a][0] = fmaf(d[a], xq.x, ap[a][0]);
+                    ap[a][1] = fmaf(d[a], xq.y, ap[a][1]);
+                    ap[a][2] = fmaf(d[a], xq.z, ap[a][2]);
+                    ap[a][3] = fmaf(d[a], xq.w, ap[a][3]);
+                    ab[a] += d[a];
                 }
             }
         }
     }
+    // reduce the 5 token classes of dW_qkv through LDS, then write the partial row
+    __syncthreads();
+    float* red = sm;  // [250][16]
+    if (threadIdx.x < 250) {
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+            *reinterpret_cast<float4*>(red + threadIdx.x * 16 + 4 * a) =
+                make_float4(aq[a][0], aq[a][1], aq[a][2], aq[a][3]);
+    }
+    __syncthreads();
     float* out = partial + (size_t)blockIdx.x * kGradLen;
-    if (threadIdx.x < kQkvQuads) {
-        const int r = threadIdx.x / (kEmb / 4), c4 = threadIdx.x % (kEmb / 4);
-        *reinterpret_cast<float4*>(out + kGQ + r * kEmb + 4 * c4) = make_float4(aq[0], aq[1], aq[2], aq[3]);
-    }
+    for (int e = threadIdx.x; e < (2 * kKq + kEmb) * kEmb; e += kBwdThreads) {
+        const int r = e / kEmb, c = e % kEmb;
+        const int tile = (r / 4) * 5 + c / 4, within = (r % 4) * 4 + (c % 4);
+        float acc = 0.f;
 #pragma unroll
-    for (int u = 0; u < kP1; u++) {
-        const int e = threadIdx.x + u * kBwdThreads;
-        if (e < kPQuads) {
-            *reinterpret_cast<float4*>(out + kGP + e * kPin) = make_float4(ap[u][0], ap[u][1], ap[u][2], ap[u][3]);
-            out[kGB + e] = ab[u];
+        for (int k = 0; k < 5; k++) acc += red[(tile * 5 + k) * 16 + within];
+        out[kGQ + e] = acc;
+    }
+    if (threadIdx.x < kTok * (kEmb / 4)) {
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+            const int e = ptk * kEmb + pc0 + a;
+            *reinterpret_cast<float4*>(out + kGP + e * kPin) = make_float4(ap[a][0], ap[a][1], ap[a][2], ap[a][3]);
+            out[kGB + e] = ab[a];
         }
     }
 }
