@@ -159,22 +159,29 @@ int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t*
 
 /* Actor front-end, fused (networks.py:31-34,51-82): the 23 feature embeddings
  * (Projection; parity != 0 keeps quirk Q1, every embedding reads x[:, 0:d_i]),
- * Q/K/V, softmax(QK^T/sqrt(10))V and the residual, for B rows of x [B, ldx]
- * (ldx >= 65).  Weights: wp [23,20,4] (embedding i's Linear weight zero-padded
- * to 4 inputs), bp [23,20], wq/wk [10,20], wv [20,20] (nn.Linear layout).
- * Output h [B, 460] f32. */
-int mm_actor_front_fwd(const float* wp, const float* bp, const float* wq, const float* wk, const float* wv,
-                       const float* x, int ldx, int B, int parity, float* h, void* stream);
+ * Q/K/V, softmax(QK^T/sqrt(10))V and the residual.
+ *
+ * mm_actor_front_prep: builds the workspace ws [mm_actor_front_ws_len()] from
+ * the parameters -- wproj/bproj: HOST arrays of the 23 device pointers of
+ * projection.layers[i].weight [20, d_i] / .bias [20]; wq/wk [10,20], wv
+ * [20,20] (nn.Linear layout).  Call again whenever the parameters change.
+ * mm_actor_front_fwd: h [B, 460] f32 for B rows of x [B, ldx] (ldx >= 65). */
+int mm_actor_front_ws_len(void);
+int mm_actor_front_prep(const float* const* wproj, const float* const* bproj, const float* wq, const float* wk,
+                        const float* wv, float* ws, void* stream);
+int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h, void* stream);
 
 /* Backward of mm_actor_front_fwd for the upstream gradient dh [B, 460]: a
- * persistent grid of `grid` workgroups, each writing one row of
- * partial [grid, mm_actor_front_grad_len()] = its rows' weight gradients laid
- * out as [dwq 10x20 | dwk 10x20 | dwv 20x20 | dwp 23x20x4 | dbp 23x20]; the
- * caller sums the rows (deterministic: fixed row -> workgroup map). */
+ * persistent grid of `grid` workgroups (2 per CU is the design point), each
+ * writing one row of partial [grid, mm_actor_front_partial_len()]; the rows
+ * are then summed into red [mm_actor_front_partial_len()] and turned into
+ * grad [mm_actor_front_grad_len()] = [dwq 10x20 | dwk 10x20 | dwv 20x20 |
+ * dwp 23x20x4 (embedding i's weight gradient zero-padded to 4 inputs) |
+ * dbp 23x20].  Every sum has a fixed order (deterministic). */
 int mm_actor_front_grad_len(void);
-int mm_actor_front_bwd(const float* wp, const float* bp, const float* wq, const float* wk, const float* wv,
-                       const float* x, int ldx, int B, int parity, const float* dh, float* partial, int grid,
-                       void* stream);
+int mm_actor_front_partial_len(void);
+int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int parity, const float* dh, float* partial,
+                       int grid, float* red, float* grad, void* stream);
 
 #ifdef __cplusplus
 }

@@ -4,20 +4,29 @@
 //
 // Why fused: per sample the front-end is a chain of 23x20 / 23x23 matrices.
 // As library calls it becomes batched GEMMs with 10..23-wide tiles plus
-// [B,23,40] split/cat copies -- the dominant cost of the PPO update.  Here a
-// 32-lane group owns one sample, lane i = token i (23 of 32 lanes active):
-// its embedding t_i and q_i stay in registers; every token's k, v (and in the
-// backward q, P, dS, dctx) sit in LDS and are read as wave-wide broadcasts
-// with 16-byte reads; the Q/K/V weights are staged once per workgroup in LDS.
-// fp32 throughout (fmaf accumulation; the reference's op order per element:
-// logits / sqrt(10), softmax = exp(x - max) / sum).
+// [B,23,40] split/cat copies.  Here a 32-lane group owns one sample, lane i =
+// token i (23 of 32 lanes active): its own vectors stay in registers, every
+// token's k, v (and in the backward q, P, dS) sit in LDS and are read as
+// broadcasts.  fp32 throughout (fmaf accumulation; the reference's op order
+// per element: logits / sqrt(10), softmax = exp(x - max) * (1 / sum)).
 //
+// Linear-map folding.  Token i's input is a <= 4-wide slice x_i, and
+//   t_i = Wp_i x_i + b_i,   [q|k|v]_i = Wqkv t_i = (Wqkv Wp_i) x_i + Wqkv b_i,
+// so k_front_prep folds A_i = Wqkv Wp_i [40x4] and c_i = Wqkv b_i once per
+// call (parameters are fixed within a forward/backward), and the kernels
+// form q, k, v with 4 FMAs per output instead of 20.  In the backward the
+// gradient of t_i is only needed for dWp_i = sum dt x^T and dbp_i = sum dt, and
+// dt = dctx + Wqkv^T g (g = [dq|dk|dv]), so the kernel accumulates
+// E_i = sum g x^T, F_i = sum dctx x^T, e_i = sum g, f_i = sum dctx and
+// k_front_combine applies Wqkv^T once at the end.
+//
+// Workspace (k_front_prep): [Wp 23x20x4 | bp 23x20 | A 23x40x4 | c 23x40 | Wqkv 40x20]
 // Forward : x [B, ldx] -> h [B, 460] = t + softmax(q k^T / sqrt(10)) v
-// Backward: persistent grid; each workgroup accumulates the weight gradients
-//           of the rows it owns in registers (fixed entry -> thread map, so the
-//           sum order is deterministic) and writes ONE partial row of
-//           kGradLen floats; the caller sums the partial rows.  Sized for two
-//           256-thread workgroups per CU (grid = 2 x CUs).
+// Backward: persistent grid of 256-thread workgroups (8 samples per
+//           iteration, two workgroups per CU); fixed entry -> thread maps, so
+//           every sum has a fixed order (deterministic).  Each workgroup writes
+//           one partial row; k_front_sum adds the rows, k_front_combine forms
+//           the parameter gradients.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -29,36 +38,47 @@ namespace mm {
 constexpr int kTok = 23;            // FEATURE_AMOUNT
 constexpr int kEmb = 20;            // EMBEDDING_DIM
 constexpr int kKq = 10;             // kq_dim
+constexpr int kQkv = 2 * kKq + kEmb;  // 40 rows of [wq; wk; wv]
 constexpr int kPin = 4;             // max feature width (networks.py:8)
 constexpr int kRowF = kTok * kEmb;  // 460
 constexpr float kSqrtKq = 3.16227766016838f;  // f32(np.sqrt(10)): the reference divides by it
+constexpr float kRSqrtKq = 0.316227766016838f;  // RN(1 / kSqrtKq)
 
-// gradient partial layout: [wq 10x20 | wk 10x20 | wv 20x20 | wp 23x20x4 | bp 23x20]
-constexpr int kGQ = 0, kGK = 200, kGV = 400, kGP = 800, kGB = 800 + kTok * kEmb * kPin;
+// x / sqrt(10): reciprocal product plus one fma residual correction (Markstein),
+// which lands on the correctly rounded quotient -- 3 VALU ops instead of a
+// full IEEE division sequence
+__device__ __forceinline__ float div_sqrt_kq(float x) {
+    const float q = x * kRSqrtKq;
+    return fmaf(fmaf(-q, kSqrtKq, x), kRSqrtKq, q);
+}
+
+// workspace (floats)
+constexpr int kWsWP = 0;                          // [23][20][4], zero beyond d_i
+constexpr int kWsBP = kWsWP + kTok * kEmb * kPin;  // [23][20]
+constexpr int kWsA = kWsBP + kTok * kEmb;          // [23][40][4]
+constexpr int kWsC = kWsA + kTok * kQkv * kPin;    // [23][40]
+constexpr int kWsW = kWsC + kTok * kQkv;           // [40][20]
+constexpr int kWsLen = kWsW + kQkv * kEmb;         // 7700
+
+// backward partial row (floats)
+constexpr int kGd = kQkv + kEmb;                    // 60 rows per token: g (40) then dctx (20)
+constexpr int kPQkv = 0;                            // dWqkv [40][20]
+constexpr int kPEF = kPQkv + kQkv * kEmb;           // [23][60][4]: E_i (rows 0-39), F_i (rows 40-59)
+constexpr int kPef = kPEF + kTok * kGd * kPin;      // [23][60]: e_i, f_i
+constexpr int kPartLen = kPef + kTok * kGd;         // 7700
+
+// final gradient layout: [wq 10x20 | wk 10x20 | wv 20x20 | wp 23x20x4 | bp 23x20]
+constexpr int kGP = kQkv * kEmb, kGB = kGP + kTok * kEmb * kPin;
 constexpr int kGradLen = kGB + kTok * kEmb;  // 3100
 
 __constant__ int c_dims[kTok] = {4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 2, 2, 1, 4, 1, 1, 1, 1, 1, 1, 2};
 __constant__ int c_starts_fixed[kTok] = {0,  4,  8,  12, 16, 20, 24, 28, 32, 36, 40, 44,
                                          48, 50, 52, 53, 57, 58, 59, 60, 61, 62, 63};
 
-struct FrontW {
-    const float* wp;  // [23][20][4] per-token projection weights, zero beyond d_i
-    const float* bp;  // [23][20]
-    const float* wq;  // [10][20]  (nn.Linear weight: [out, in])
-    const float* wk;  // [10][20]
-    const float* wv;  // [20][20]
+struct ProjPtrs {  // the 23 Linear(d_i -> 20) modules' parameters (nn.Linear layout [20][d_i], [20])
+    const float* w[kTok];
+    const float* b[kTok];
 };
-
-struct WLds {  // Q/K/V weights: [40][20] = rows of wq, wk, wv
-    float w[2 * kKq + kEmb][kEmb];
-};
-
-__device__ __forceinline__ void stage_w(const FrontW& W, WLds& s) {
-    for (int e = threadIdx.x; e < (2 * kKq + kEmb) * kEmb; e += blockDim.x) {
-        const int r = e / kEmb, c = e % kEmb;
-        s.w[r][c] = r < kKq ? W.wq[e] : (r < 2 * kKq ? W.wk[e - kKq * kEmb] : W.wv[e - 2 * kKq * kEmb]);
-    }
-}
 
 // x slice of token i (zero beyond d_i)
 __device__ __forceinline__ float4 xslice(const float* __restrict__ xr, int i, bool parity) {
@@ -67,56 +87,37 @@ __device__ __forceinline__ float4 xslice(const float* __restrict__ xr, int i, bo
     return make_float4(xr[s], d > 1 ? xr[s + 1] : 0.f, d > 2 ? xr[s + 2] : 0.f, d > 3 ? xr[s + 3] : 0.f);
 }
 
-// Token embedding t_i = W_i x_i + b_i (Projection; quirk Q1 when parity)
-__device__ __forceinline__ void embed(const FrontW& W, float4 xv, int i, float t[kEmb]) {
-    const float4* wi = reinterpret_cast<const float4*>(W.wp) + i * kEmb;
+// o[r] = M[r] . xv + c[r] for the rows r of a [R][4] matrix (per-lane rows;
+// M and c 16-byte aligned, R % 4 == 0)
+template <int R>
+__device__ __forceinline__ void affine4(const float* __restrict__ M, const float* __restrict__ c, float4 xv,
+                                        float o[R]) {
+    const float4* m4 = reinterpret_cast<const float4*>(M);
+    const float4* c4 = reinterpret_cast<const float4*>(c);
 #pragma unroll
-    for (int c = 0; c < kEmb; c++) {
-        const float4 w = wi[c];
-        float acc = w.x * xv.x;
-        acc = fmaf(w.y, xv.y, acc);
-        acc = fmaf(w.z, xv.z, acc);
-        acc = fmaf(w.w, xv.w, acc);
-        t[c] = acc + W.bp[i * kEmb + c];
-    }
-}
-
-// Weights read by every lane alike go through the scalar cache: a pointer in
-// the constant address space makes the uniform loads s_load_dword* into SGPRs
-// that the FMAs take as their scalar operand (no LDS traffic, no VGPRs).
-typedef const __attribute__((address_space(4))) float cfloat;
-__device__ __forceinline__ cfloat* as_const(const float* p) { return (cfloat*)p; }
-
-// o[a] = sum_b w[a][b] t[b], w = [OUT][20] row-major in global memory (scalar loads)
-template <int OUT>
-__device__ __forceinline__ void matvec_s(const float* w, const float t[kEmb], float o[OUT]) {
-    cfloat* ws = as_const(w);
+    for (int r4 = 0; r4 < R / 4; r4++) {
+        const float4 cv = c4[r4];
+        const float cc[4] = {cv.x, cv.y, cv.z, cv.w};
 #pragma unroll
-    for (int a = 0; a < OUT; a++) {
-        float acc = 0.f;
-#pragma unroll
-        for (int b = 0; b < kEmb; b++) acc = fmaf(ws[a * kEmb + b], t[b], acc);
-        o[a] = acc;
-    }
-}
-
-// o[a] = sum_b w[r0 + a][b] t[b]
-template <int OUT>
-__device__ __forceinline__ void matvec(const WLds& s, int r0, const float t[kEmb], float o[OUT]) {
-#pragma unroll
-    for (int a = 0; a < OUT; a++) {
-        const float4* w4 = reinterpret_cast<const float4*>(s.w[r0 + a]);
-        float acc = 0.f;
-#pragma unroll
-        for (int b = 0; b < kEmb / 4; b++) {
-            const float4 w = w4[b];
-            acc = fmaf(w.x, t[4 * b], acc);
-            acc = fmaf(w.y, t[4 * b + 1], acc);
-            acc = fmaf(w.z, t[4 * b + 2], acc);
-            acc = fmaf(w.w, t[4 * b + 3], acc);
+        for (int u = 0; u < 4; u++) {
+            const float4 w = m4[4 * r4 + u];
+            float acc = w.x * xv.x;
+            acc = fmaf(w.y, xv.y, acc);
+            acc = fmaf(w.z, xv.z, acc);
+            acc = fmaf(w.w, xv.w, acc);
+            o[4 * r4 + u] = acc + cc[u];
         }
-        o[a] = acc;
     }
+}
+
+// token embedding t_i = Wp_i x_i + b_i (Projection; quirk Q1 when parity)
+__device__ __forceinline__ void embed(const float* __restrict__ ws, float4 xv, int i, float t[kEmb]) {
+    affine4<kEmb>(ws + kWsWP + i * kEmb * kPin, ws + kWsBP + i * kEmb, xv, t);
+}
+
+// [q|k|v] of token i from its input slice (folded maps)
+__device__ __forceinline__ void qkv_of(const float* __restrict__ ws, float4 xv, int i, float o[kQkv]) {
+    affine4<kQkv>(ws + kWsA + i * kQkv * kPin, ws + kWsC + i * kQkv, xv, o);
 }
 
 template <int N>
@@ -168,32 +169,80 @@ __device__ __forceinline__ void axpy4(float* acc, float p, const float* __restri
 }
 
 // ---------------------------------------------------------------------------
+// prep: workspace from the parameters (one workgroup per token)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_front_prep(ProjPtrs P, const float* __restrict__ wq,
+                                                    const float* __restrict__ wk, const float* __restrict__ wv,
+                                                    float* __restrict__ ws) {
+    __shared__ float W[kQkv][kEmb];
+    __shared__ float Wp[kEmb][kPin];
+    __shared__ float bp[kEmb];
+    const int i = blockIdx.x;
+    const int d = c_dims[i];
+    const float* wi = P.w[0];
+    const float* bi = P.b[0];
+#pragma unroll
+    for (int k = 1; k < kTok; k++)  // uniform select (no dynamic indexing of the argument struct)
+        if (k == i) {
+            wi = P.w[k];
+            bi = P.b[k];
+        }
+    for (int e = threadIdx.x; e < kQkv * kEmb; e += blockDim.x) {
+        const int r = e / kEmb;
+        const float w = r < kKq ? wq[e] : (r < 2 * kKq ? wk[e - kKq * kEmb] : wv[e - 2 * kKq * kEmb]);
+        W[r][e % kEmb] = w;
+        if (i == 0) ws[kWsW + e] = w;
+    }
+    for (int e = threadIdx.x; e < kEmb * kPin; e += blockDim.x) {
+        const int c = e / kPin, k = e % kPin;
+        const float w = k < d ? wi[c * d + k] : 0.f;
+        Wp[c][k] = w;
+        ws[kWsWP + i * kEmb * kPin + e] = w;
+    }
+    for (int c = threadIdx.x; c < kEmb; c += blockDim.x) {
+        bp[c] = bi[c];
+        ws[kWsBP + i * kEmb + c] = bi[c];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < kQkv * kPin; e += blockDim.x) {  // A_i = Wqkv Wp_i
+        const int r = e / kPin, k = e % kPin;
+        float acc = 0.f;
+        for (int c = 0; c < kEmb; c++) acc = fmaf(W[r][c], Wp[c][k], acc);
+        ws[kWsA + i * kQkv * kPin + e] = acc;
+    }
+    for (int r = threadIdx.x; r < kQkv; r += blockDim.x) {  // c_i = Wqkv b_i
+        float acc = 0.f;
+        for (int c = 0; c < kEmb; c++) acc = fmaf(W[r][c], bp[c], acc);
+        ws[kWsC + i * kQkv + r] = acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
 constexpr int kFwdRows = 8;  // samples per 256-thread workgroup
 
-__global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __restrict__ x, int ldx, int B,
-                                                   int parity, float* __restrict__ h) {
+__global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws, const float* __restrict__ x,
+                                                   int ldx, int B, int parity, float* __restrict__ h) {
     __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKq];
     __shared__ __attribute__((aligned(16))) float Vs[kFwdRows][kTok][kEmb];
-    __shared__ __attribute__((aligned(16))) WLds Ws;
-    stage_w(W, Ws);
-    __syncthreads();
     const int g = threadIdx.x >> 5;  // sample slot in the workgroup
     const int i = threadIdx.x & 31;  // token
     const int row = blockIdx.x * kFwdRows + g;
     const bool act = (i < kTok) && (row < B);
-    float t[kEmb], q[kKq];
+    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+    float q[kKq];
     if (act) {
-        embed(W, xslice(x + (size_t)row * ldx, i, parity != 0), i, t);
-        float k[kKq], v[kEmb];
-        matvec<kKq>(Ws, 0, t, q);
-        matvec<kKq>(Ws, kKq, t, k);
-        matvec<kEmb>(Ws, 2 * kKq, t, v);
+        xv = xslice(x + (size_t)row * ldx, i, parity != 0);
+        float o[kQkv];
+        qkv_of(ws, xv, i, o);
 #pragma unroll
-        for (int a = 0; a < kKq; a++) Ks[g][i][a] = k[a];
+        for (int a = 0; a < kKq; a++) {
+            q[a] = o[a];
+            Ks[g][i][a] = o[kKq + a];
+        }
 #pragma unroll
-        for (int a = 0; a < kEmb; a++) Vs[g][i][a] = v[a];
+        for (int c = 0; c < kEmb; c++) Vs[g][i][c] = o[2 * kKq + c];
     }
     __syncthreads();
     if (!act) return;
@@ -201,7 +250,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __rest
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < kTok; j++) {
-        s[j] = dot4<kKq>(q, Ks[g][j]) / kSqrtKq;
+        s[j] = div_sqrt_kq(dot4<kKq>(q, Ks[g][j]));
         mx = fmaxf(mx, s[j]);
     }
     float sum = 0.f;
@@ -213,8 +262,11 @@ __global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __rest
     float out[kEmb];
 #pragma unroll
     for (int c = 0; c < kEmb; c++) out[c] = 0.f;
+    const float inv = 1.f / sum;  // torch's softmax scales by the reciprocal of the sum
 #pragma unroll
-    for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] / sum, Vs[g][j]);
+    for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] * inv, Vs[g][j]);
+    float t[kEmb];
+    embed(ws, xv, i, t);
     float* o = h + (size_t)row * kRowF + i * kEmb;
 #pragma unroll
     for (int c = 0; c < kEmb; c += 4)
@@ -225,57 +277,54 @@ __global__ __launch_bounds__(256) void k_front_fwd(FrontW W, const float* __rest
 // ---------------------------------------------------------------------------
 // backward (persistent, in-kernel weight-gradient reduction)
 // ---------------------------------------------------------------------------
-// 256 threads = 8 samples per iteration (32-lane group g = sample, lane i =
-// token).  LDS per sample (floats): attention phase {K 23x10 | Q 23x10 |
-// V 23x20 | P 23x23 | dS 23x23}; after a barrier the same words hold the
-// weight-gradient operands {G = [dq|dk|dv] 23x40 | T 23x20 | dT 23x20 | X 23x4}.
-// dctx rows are re-read from global (L1/L2) rather than staged.  With the
-// Q/K/V weights that is 66.5 KB per workgroup: two workgroups (8 waves) per CU.
+// LDS per sample (floats): attention phase {K 23x10 | Q 23x10 | V 23x20 |
+// P 23x23 | dS 23x23}; after a barrier the same words hold the reduction
+// operands {G = [dq|dk|dv] 23x40 | T 23x20 | dctx 23x20 | X 23x4}.  dctx rows
+// of other tokens are re-read from global (L1/L2) in phase 3.  63 KB per
+// workgroup: two workgroups (8 waves) per CU.
 constexpr int kBwdRows = 8;
 constexpr int kBwdThreads = 256;
 constexpr int kOffK = 0, kOffQ = 230, kOffV = 460, kOffP = 920, kOffS = 1449;  // attention phase
-constexpr int kOffG = 0, kOffT = 920, kOffD = 1380, kOffX = 1840;               // weight-gradient phase
+constexpr int kOffG = 0, kOffT = 920, kOffD = 1380, kOffX = 1840;               // reduction phase
 constexpr int kSampleF = 1980;  // floats per sample (>= 1978 and >= 1932; multiple of 4)
-constexpr int kQkvQuads = (2 * kKq + kEmb) * (kEmb / 4);  // 200 (row a, columns 4b..4b+3) of [40 x 20]
-constexpr int kPQuads = kTok * kEmb;                      // 460 (token i, channel c) x 4 inputs
-constexpr int kP1 = (kPQuads + kBwdThreads - 1) / kBwdThreads;  // 2
+constexpr int kQkvTiles = (kQkv / 4) * (kEmb / 4);  // 50 4x4 tiles of dWqkv
+constexpr int kClasses = 5;                          // token classes j mod 5 per tile
+constexpr int kEFUnits = kTok * (kGd / 4);           // 345 (token, 4 rows of [g|dctx])
 
-__global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const float* __restrict__ x, int ldx, int B,
+__global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __restrict__ ws,
+                                                              const float* __restrict__ x, int ldx, int B,
                                                               int parity, const float* __restrict__ dh,
                                                               float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kSampleF];
     const int g = threadIdx.x >> 5;
     const int i = threadIdx.x & 31;
     float* my = sm + g * kSampleF;
-    // weight-gradient accumulators, fixed entry map (deterministic sums):
-    //   dW_qkv [40 x 20] as 50 4x4 tiles x 5 token classes (j mod 5): thread t < 250
-    //   dW_p / db_p: (token, 4 channels) units: thread t < 115
-    const int qt = threadIdx.x / 5, qc = threadIdx.x % 5;  // tile (rows 4*(qt/5).., cols 4*(qt%5)..), token class
-    const int qr0 = 4 * (qt / 5), qc0 = 4 * (qt % 5);
+    // dWqkv: thread t < 250 owns 4x4 tile t / 5 for tokens j = t % 5 (mod 5)
+    const int qt = threadIdx.x / kClasses, qc = threadIdx.x % kClasses;
+    const int qr0 = 4 * (qt / (kEmb / 4)), qc0 = 4 * (qt % (kEmb / 4));
     float aq[4][4];
 #pragma unroll
     for (int a = 0; a < 4; a++) aq[a][0] = aq[a][1] = aq[a][2] = aq[a][3] = 0.f;
-    const int ptk = threadIdx.x / 5, pc0 = 4 * (threadIdx.x % 5);  // token, first channel
-    float ap[4][4], ab[4];
+    // E/F/e/f: thread t owns units t and t + 256 (token u / 15, rows 4 (u % 15) ..)
+    float ae[2][4][4], as[2][4];
 #pragma unroll
-    for (int a = 0; a < 4; a++) ap[a][0] = ap[a][1] = ap[a][2] = ap[a][3] = ab[a] = 0.f;
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int a = 0; a < 4; a++) ae[u][a][0] = ae[u][a][1] = ae[u][a][2] = ae[u][a][3] = as[u][a] = 0.f;
     const int iters = (B + kBwdRows - 1) / kBwdRows;
     for (int it = blockIdx.x; it < iters; it += gridDim.x) {
         const int row0 = it * kBwdRows;
         const int nrow = min(kBwdRows, B - row0);
         const int row = row0 + g;
         const bool act = (i < kTok) && (g < nrow);
-        __syncthreads();  // previous iteration's weight-gradient readers are done
+        __syncthreads();  // previous iteration's reduction readers are done
         float dctx[kEmb];
         float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
         const float* dhr = dh + (size_t)row * kRowF;
-        if (act) {  // phase 1: embedding, q/k/v
+        if (act) {  // phase 1: q/k/v (folded maps), own dctx row
             xv = xslice(x + (size_t)row * ldx, i, parity != 0);
-            float t[kEmb], q[kKq], k[kKq], v[kEmb];
-            embed(W, xv, i, t);
-            matvec_s<kKq>(W.wq, t, q);
-            matvec_s<kKq>(W.wk, t, k);
-            matvec_s<kEmb>(W.wv, t, v);
+            float o[kQkv];
+            qkv_of(ws, xv, i, o);
 #pragma unroll
             for (int c = 0; c < kEmb; c += 4) {
                 const float4 d4 = *reinterpret_cast<const float4*>(dhr + i * kEmb + c);
@@ -286,12 +335,13 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
             }
 #pragma unroll
             for (int a = 0; a < kKq; a += 2) {
-                *reinterpret_cast<float2*>(my + kOffK + i * kKq + a) = make_float2(k[a], k[a + 1]);
-                *reinterpret_cast<float2*>(my + kOffQ + i * kKq + a) = make_float2(q[a], q[a + 1]);
+                *reinterpret_cast<float2*>(my + kOffQ + i * kKq + a) = make_float2(o[a], o[a + 1]);
+                *reinterpret_cast<float2*>(my + kOffK + i * kKq + a) = make_float2(o[kKq + a], o[kKq + a + 1]);
             }
 #pragma unroll
             for (int c = 0; c < kEmb; c += 4)
-                *reinterpret_cast<float4*>(my + kOffV + i * kEmb + c) = make_float4(v[c], v[c + 1], v[c + 2], v[c + 3]);
+                *reinterpret_cast<float4*>(my + kOffV + i * kEmb + c) =
+                    make_float4(o[2 * kKq + c], o[2 * kKq + c + 1], o[2 * kKq + c + 2], o[2 * kKq + c + 3]);
         }
         __syncthreads();
         float dq[kKq];
@@ -307,7 +357,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                p[j] = dot4<kKq>(q, my + kOffK + j * kKq) / kSqrtKq;
+                p[j] = div_sqrt_kq(dot4<kKq>(q, my + kOffK + j * kKq));
                 mx = fmaxf(mx, p[j]);
             }
             float sum = 0.f;
@@ -318,9 +368,10 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
             }
             float dp[kTok];
             float rs = 0.f;
+            const float inv = 1.f / sum;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                p[j] = p[j] / sum;
+                p[j] = p[j] * inv;
                 dp[j] = dot4<kEmb>(dctx, my + kOffV + j * kEmb);  // dP_ij = dctx_i . v_j
                 rs = fmaf(dp[j], p[j], rs);
             }
@@ -328,15 +379,15 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
             for (int a = 0; a < kKq; a++) dq[a] = 0.f;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                const float ds = (p[j] * (dp[j] - rs)) / kSqrtKq;  // softmax backward, then / sqrt(10)
+                const float ds = div_sqrt_kq(p[j] * (dp[j] - rs));  // softmax backward, then / sqrt(10)
                 my[kOffP + i * kTok + j] = p[j];
                 my[kOffS + i * kTok + j] = ds;
                 axpy4<kKq>(dq, ds, my + kOffK + j * kKq);
             }
         }
         __syncthreads();
-        float dk[kKq], dv[kEmb], dt[kEmb], t[kEmb];
-        if (act) {  // phase 3: dv_i = sum_j P_ji dctx_j, dk_i = sum_j dS_ji q_j, dt_i
+        float dk[kKq], dv[kEmb];
+        if (act) {  // phase 3: dv_i = sum_j P_ji dctx_j, dk_i = sum_j dS_ji q_j
 #pragma unroll
             for (int c = 0; c < kEmb; c++) dv[c] = 0.f;
 #pragma unroll
@@ -356,29 +407,12 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
                 }
                 axpy4<kKq>(dk, sj, my + kOffQ + j * kKq);
             }
-            // dt_i = dctx_i (residual) + Wq^T dq + Wk^T dk + Wv^T dv (scalar-loaded weights)
-            cfloat* wq = as_const(W.wq);
-            cfloat* wk = as_const(W.wk);
-            cfloat* wv = as_const(W.wv);
-#pragma unroll
-            for (int b = 0; b < kEmb; b++) dt[b] = dctx[b];
-#pragma unroll
-            for (int r = 0; r < kKq; r++)
-#pragma unroll
-                for (int b = 0; b < kEmb; b++) dt[b] = fmaf(dq[r], wq[r * kEmb + b], dt[b]);
-#pragma unroll
-            for (int r = 0; r < kKq; r++)
-#pragma unroll
-                for (int b = 0; b < kEmb; b++) dt[b] = fmaf(dk[r], wk[r * kEmb + b], dt[b]);
-#pragma unroll
-            for (int r = 0; r < kEmb; r++)
-#pragma unroll
-                for (int b = 0; b < kEmb; b++) dt[b] = fmaf(dv[r], wv[r * kEmb + b], dt[b]);
         }
-        __syncthreads();  // attention-phase words are dead: reuse them for the gradient operands
+        __syncthreads();  // attention-phase words are dead: reuse them for the reduction operands
         if (act) {
-            embed(W, xv, i, t);  // recomputed rather than held in registers through phases 2-3
-            float* G = my + kOffG + i * (2 * kKq + kEmb);
+            float t[kEmb];
+            embed(ws, xv, i, t);
+            float* G = my + kOffG + i * kQkv;
 #pragma unroll
             for (int a = 0; a < kKq; a += 2) {
                 *reinterpret_cast<float2*>(G + a) = make_float2(dq[a], dq[a + 1]);
@@ -389,17 +423,17 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
                 *reinterpret_cast<float4*>(G + 2 * kKq + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
                 *reinterpret_cast<float4*>(my + kOffT + i * kEmb + c) = make_float4(t[c], t[c + 1], t[c + 2], t[c + 3]);
                 *reinterpret_cast<float4*>(my + kOffD + i * kEmb + c) =
-                    make_float4(dt[c], dt[c + 1], dt[c + 2], dt[c + 3]);
+                    make_float4(dctx[c], dctx[c + 1], dctx[c + 2], dctx[c + 3]);
             }
             *reinterpret_cast<float4*>(my + kOffX + i * kPin) = xv;
         }
         __syncthreads();
-        // phase 4: weight gradients of this iteration's nrow samples (4x4 register tiles)
-        if (threadIdx.x < 250) {
+        // phase 4a: dWqkv += G^T T over this iteration's tokens (4x4 register tiles)
+        if (threadIdx.x < kQkvTiles * kClasses) {
             for (int gg = 0; gg < nrow; gg++) {
                 const float* sg = sm + gg * kSampleF;
-                for (int j = qc; j < kTok; j += 5) {
-                    const float4 gv = *reinterpret_cast<const float4*>(sg + kOffG + j * (2 * kKq + kEmb) + qr0);
+                for (int j = qc; j < kTok; j += kClasses) {
+                    const float4 gv = *reinterpret_cast<const float4*>(sg + kOffG + j * kQkv + qr0);
                     const float4 tv = *reinterpret_cast<const float4*>(sg + kOffT + j * kEmb + qc0);
                     const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
@@ -412,49 +446,92 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
                 }
             }
         }
-        if (threadIdx.x < kTok * (kEmb / 4)) {
-            for (int gg = 0; gg < nrow; gg++) {
-                const float* sg = sm + gg * kSampleF;
-                const float4 dv4 = *reinterpret_cast<const float4*>(sg + kOffD + ptk * kEmb + pc0);
-                const float4 xq = *reinterpret_cast<const float4*>(sg + kOffX + ptk * kPin);
-                const float d[4] = {dv4.x, dv4.y, dv4.z, dv4.w};
+        // phase 4b: E/F (+= [g|dctx] x^T) and e/f (+= [g|dctx]) per token
 #pragma unroll
-                for (int a = 0; a < 4; a++) {
-                    ap[a][0] = fmaf(d[a], xq.x, ap[a][0]);
-                    ap[a][1] = fmaf(d[a], xq.y, ap[a][1]);
-                    ap[a][2] = fmaf(d[a], xq.z, ap[a][2]);
-                    ap[a][3] = fmaf(d[a], xq.w, ap[a][3]);
-                    ab[a] += d[a];
+        for (int u = 0; u < 2; u++) {
+            const int unit = threadIdx.x + u * kBwdThreads;
+            if (unit < kEFUnits) {
+                const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
+                const int off = r0 < kQkv ? kOffG + tk * kQkv + r0 : kOffD + tk * kEmb + (r0 - kQkv);
+                for (int gg = 0; gg < nrow; gg++) {
+                    const float* sg = sm + gg * kSampleF;
+                    const float4 gv = *reinterpret_cast<const float4*>(sg + off);
+                    const float4 xq = *reinterpret_cast<const float4*>(sg + kOffX + tk * kPin);
+                    const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                    for (int a = 0; a < 4; a++) {
+                        ae[u][a][0] = fmaf(gr[a], xq.x, ae[u][a][0]);
+                        ae[u][a][1] = fmaf(gr[a], xq.y, ae[u][a][1]);
+                        ae[u][a][2] = fmaf(gr[a], xq.z, ae[u][a][2]);
+                        ae[u][a][3] = fmaf(gr[a], xq.w, ae[u][a][3]);
+                        as[u][a] += gr[a];
+                    }
                 }
             }
         }
     }
-    // reduce the 5 token classes of dW_qkv through LDS, then write the partial row
+    // reduce the 5 token classes of dWqkv through LDS, then write the partial row
     __syncthreads();
     float* red = sm;  // [250][16]
-    if (threadIdx.x < 250) {
+    if (threadIdx.x < kQkvTiles * kClasses) {
 #pragma unroll
         for (int a = 0; a < 4; a++)
             *reinterpret_cast<float4*>(red + threadIdx.x * 16 + 4 * a) =
                 make_float4(aq[a][0], aq[a][1], aq[a][2], aq[a][3]);
     }
     __syncthreads();
-    float* out = partial + (size_t)blockIdx.x * kGradLen;
-    for (int e = threadIdx.x; e < (2 * kKq + kEmb) * kEmb; e += kBwdThreads) {
+    float* out = partial + (size_t)blockIdx.x * kPartLen;
+    for (int e = threadIdx.x; e < kQkv * kEmb; e += kBwdThreads) {
         const int r = e / kEmb, c = e % kEmb;
-        const int tile = (r / 4) * 5 + c / 4, within = (r % 4) * 4 + (c % 4);
+        const int tile = (r / 4) * (kEmb / 4) + c / 4, within = (r % 4) * 4 + (c % 4);
         float acc = 0.f;
 #pragma unroll
-        for (int k = 0; k < 5; k++) acc += red[(tile * 5 + k) * 16 + within];
-        out[kGQ + e] = acc;
+        for (int k = 0; k < kClasses; k++) acc += red[(tile * kClasses + k) * 16 + within];
+        out[kPQkv + e] = acc;
     }
-    if (threadIdx.x < kTok * (kEmb / 4)) {
 #pragma unroll
-        for (int a = 0; a < 4; a++) {
-            const int e = ptk * kEmb + pc0 + a;
-            *reinterpret_cast<float4*>(out + kGP + e * kPin) = make_float4(ap[a][0], ap[a][1], ap[a][2], ap[a][3]);
-            out[kGB + e] = ab[a];
+    for (int u = 0; u < 2; u++) {
+        const int unit = threadIdx.x + u * kBwdThreads;
+        if (unit < kEFUnits) {
+            const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                *reinterpret_cast<float4*>(out + kPEF + (tk * kGd + r0 + a) * kPin) =
+                    make_float4(ae[u][a][0], ae[u][a][1], ae[u][a][2], ae[u][a][3]);
+                out[kPef + tk * kGd + r0 + a] = as[u][a];
+            }
         }
+    }
+}
+
+// sum of the partial rows (fixed order over rows: deterministic)
+__global__ __launch_bounds__(256) void k_front_sum(const float* __restrict__ partial, int rows,
+                                                   float* __restrict__ red) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kPartLen) return;
+    float acc = 0.f;
+    for (int r = 0; r < rows; r++) acc += partial[(size_t)r * kPartLen + e];
+    red[e] = acc;
+}
+
+// parameter gradients: dWqkv as summed; dWp_i = F_i + Wqkv^T E_i, dbp_i = f_i + Wqkv^T e_i
+__global__ __launch_bounds__(256) void k_front_combine(const float* __restrict__ ws, const float* __restrict__ red,
+                                                       float* __restrict__ grad) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= kGradLen) return;
+    const float* W = ws + kWsW;  // [40][20]
+    if (e < kGP) {
+        grad[e] = red[kPQkv + e];
+    } else if (e < kGB) {
+        const int f = e - kGP, tk = f / (kEmb * kPin), c = (f / kPin) % kEmb, k = f % kPin;
+        float acc = red[kPEF + (tk * kGd + kQkv + c) * kPin + k];  // F_i[c][k]
+        for (int r = 0; r < kQkv; r++) acc = fmaf(W[r * kEmb + c], red[kPEF + (tk * kGd + r) * kPin + k], acc);
+        grad[e] = acc;
+    } else {
+        const int f = e - kGB, tk = f / kEmb, c = f % kEmb;
+        float acc = red[kPef + tk * kGd + kQkv + c];  // f_i[c]
+        for (int r = 0; r < kQkv; r++) acc = fmaf(W[r * kEmb + c], red[kPef + tk * kGd + r], acc);
+        grad[e] = acc;
     }
 }
 
@@ -462,26 +539,42 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(FrontW W, const fl
 
 using namespace mm;
 
-extern "C" int mm_actor_front_fwd(const float* wp, const float* bp, const float* wq, const float* wk,
-                                  const float* wv, const float* x, int ldx, int B, int parity, float* h,
+extern "C" int mm_actor_front_ws_len(void) { return kWsLen; }
+extern "C" int mm_actor_front_grad_len(void) { return kGradLen; }
+extern "C" int mm_actor_front_partial_len(void) { return kPartLen; }
+
+extern "C" int mm_actor_front_prep(const float* const* wproj, const float* const* bproj, const float* wq,
+                                   const float* wk, const float* wv, float* ws, void* stream) {
+    if (!wproj || !bproj || !wq || !wk || !wv || !ws) return MM_E_ARG;
+    ProjPtrs P;
+    for (int i = 0; i < kTok; i++) {
+        if (!wproj[i] || !bproj[i]) return MM_E_ARG;
+        P.w[i] = wproj[i];
+        P.b[i] = bproj[i];
+    }
+    hipLaunchKernelGGL(k_front_prep, dim3(kTok), dim3(256), 0, (hipStream_t)stream, P, wq, wk, wv, ws);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h,
                                   void* stream) {
-    if (!wp || !bp || !wq || !wk || !wv || !x || !h || B < 0 || ldx < MM_OBS_DIM) return MM_E_ARG;
+    if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM) return MM_E_ARG;
     if (B == 0) return 0;
-    FrontW W{wp, bp, wq, wk, wv};
-    hipLaunchKernelGGL(k_front_fwd, dim3((B + kFwdRows - 1) / kFwdRows), dim3(256), 0, (hipStream_t)stream, W, x,
+    hipLaunchKernelGGL(k_front_fwd, dim3((B + kFwdRows - 1) / kFwdRows), dim3(256), 0, (hipStream_t)stream, ws, x,
                        ldx, B, parity, h);
     return (int)hipGetLastError();
 }
 
-extern "C" int mm_actor_front_grad_len(void) { return kGradLen; }
-
-extern "C" int mm_actor_front_bwd(const float* wp, const float* bp, const float* wq, const float* wk,
-                                  const float* wv, const float* x, int ldx, int B, int parity, const float* dh,
-                                  float* partial, int grid, void* stream) {
-    if (!wp || !bp || !wq || !wk || !wv || !x || !dh || !partial || B < 0 || ldx < MM_OBS_DIM || grid <= 0)
-        return MM_E_ARG;
-    FrontW W{wp, bp, wq, wk, wv};
-    hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, (hipStream_t)stream, W, x, ldx, B, parity, dh,
-                       partial);
+extern "C" int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
+                                  float* partial, int grid, float* red, float* grad, void* stream) {
+    if (!ws || !x || !dh || !partial || !red || !grad || B < 0 || ldx < MM_OBS_DIM || grid <= 0) return MM_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_front_sum, dim3((kPartLen + 255) / 256), dim3(256), 0, s, partial, grid, red);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_front_combine, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, grad);
     return (int)hipGetLastError();
 }

@@ -33,7 +33,8 @@ AF_HAS_MARK = 64
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_env_step", "mm_env_reset_done", "mm_gae", "mm_sample",
-           "mm_actor_front_fwd", "mm_actor_front_grad_len", "mm_actor_front_bwd")
+           "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
+           "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd")
 
 
 class EnvDesc(ctypes.Structure):
@@ -81,10 +82,14 @@ def lib():
         L.mm_gae.restype = i32
         L.mm_sample.argtypes = [P, P, P, i32, u64, u64, P, P, P, P]
         L.mm_sample.restype = i32
-        L.mm_actor_front_fwd.argtypes = [P] * 6 + [i32, i32, i32, P, P]
+        L.mm_actor_front_ws_len.restype = i32
+        L.mm_actor_front_prep.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), P, P, P, P, P]
+        L.mm_actor_front_prep.restype = i32
+        L.mm_actor_front_fwd.argtypes = [P, P, i32, i32, i32, P, P]
         L.mm_actor_front_fwd.restype = i32
         L.mm_actor_front_grad_len.restype = i32
-        L.mm_actor_front_bwd.argtypes = [P] * 6 + [i32, i32, i32, P, P, i32, P]
+        L.mm_actor_front_partial_len.restype = i32
+        L.mm_actor_front_bwd.argtypes = [P, P, i32, i32, i32, P, P, i32, P, P, P]
         L.mm_actor_front_bwd.restype = i32
         _LIB = L
     return _LIB

@@ -13,6 +13,8 @@ so every embedding reads ``x[:, 0:d_i]`` and the actor sees only obs[0:4].
 ``parity_mode=True`` (default) keeps that; ``parity_mode=False`` gives each
 feature its own slice (what the code evidently intended).
 """
+import ctypes
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -84,25 +86,34 @@ def _cu_count(dev):
 
 
 class _FusedFront(torch.autograd.Function):
-    """Projection + attention + residual as one HIP kernel each way (csrc/actor_front.hip).
+    """Projection + attention + residual as HIP kernels (csrc/actor_front.hip).
 
-    The backward kernel reduces the weight gradients (sums over all B*23
-    tokens) inside a persistent grid into per-workgroup partial rows; one
-    torch sum over those rows finishes them.
+    apply(x [B, 65], parity, *params) with params = the 23 projection weights,
+    the 23 projection biases, querys, keys, values weights (module order).  A
+    tiny prep kernel folds the parameters into a workspace every call; the
+    backward kernel reduces the weight gradients inside a persistent grid and
+    two small kernels finish them (no per-parameter copies or pads).
     """
 
     @staticmethod
-    def forward(ctx, x, wp, bp, wq, wk, wv, parity):
+    def forward(ctx, x, parity, *params):
         from . import _lib
 
+        L = _lib.lib()
         B = x.shape[0]
         x = x.contiguous()
-        wp, bp, wq, wk, wv = (t.contiguous() for t in (wp, bp, wq, wk, wv))
+        ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device=x.device)
+        ptrs = [p.data_ptr() for p in params]
+        wp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
+        bp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[FEATURE_AMOUNT:2 * FEATURE_AMOUNT])
+        wq, wk, wv = params[2 * FEATURE_AMOUNT:]
+        stream = _lib.stream_ptr()
+        _lib.check(L.mm_actor_front_prep(wp, bp, _lib.ptr(wq), _lib.ptr(wk), _lib.ptr(wv), _lib.ptr(ws), stream),
+                   "mm_actor_front_prep")
         h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
-        _lib.check(_lib.lib().mm_actor_front_fwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
-                                                 int(parity), _lib.ptr(h), _lib.stream_ptr()),
+        _lib.check(L.mm_actor_front_fwd(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h), stream),
                    "mm_actor_front_fwd")
-        ctx.save_for_backward(x, wp, bp, wq, wk, wv)
+        ctx.save_for_backward(x, ws)
         ctx.parity = parity
         return h
 
@@ -110,26 +121,34 @@ class _FusedFront(torch.autograd.Function):
     def backward(ctx, dh):
         from . import _lib
 
-        x, wp, bp, wq, wk, wv = ctx.saved_tensors
+        x, ws = ctx.saved_tensors
         B = x.shape[0]
         dh = dh.contiguous()
         L = _lib.lib()
-        glen = L.mm_actor_front_grad_len()
         grid = max(1, min(2 * _cu_count(x.device), (B + 7) // 8))  # two 8-sample workgroups per CU
-        partial = torch.empty((grid, glen), dtype=torch.float32, device=x.device)
-        _lib.check(L.mm_actor_front_bwd(*(_lib.ptr(t) for t in (wp, bp, wq, wk, wv, x)), OBS_SPACE, B,
-                                        int(ctx.parity), _lib.ptr(dh), _lib.ptr(partial), grid, _lib.stream_ptr()),
+        plen = L.mm_actor_front_partial_len()
+        partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
+        red = torch.empty(plen, dtype=torch.float32, device=x.device)
+        g = torch.empty(L.mm_actor_front_grad_len(), dtype=torch.float32, device=x.device)
+        _lib.check(L.mm_actor_front_bwd(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(ctx.parity), _lib.ptr(dh),
+                                        _lib.ptr(partial), grid, _lib.ptr(red), _lib.ptr(g), _lib.stream_ptr()),
                    "mm_actor_front_bwd")
-        g = partial.sum(0)
         n_qk, n_v = KQ_DIM * EMBEDDING_DIM, EMBEDDING_DIM * EMBEDDING_DIM
-        n_p = FEATURE_AMOUNT * EMBEDDING_DIM * 4
         dwq = g[0:n_qk].view(KQ_DIM, EMBEDDING_DIM)
         dwk = g[n_qk:2 * n_qk].view(KQ_DIM, EMBEDDING_DIM)
         dwv = g[2 * n_qk:2 * n_qk + n_v].view(EMBEDDING_DIM, EMBEDDING_DIM)
         o = 2 * n_qk + n_v
+        n_p = FEATURE_AMOUNT * EMBEDDING_DIM * 4
         dwp = g[o:o + n_p].view(FEATURE_AMOUNT, EMBEDDING_DIM, 4)
         dbp = g[o + n_p:].view(FEATURE_AMOUNT, EMBEDDING_DIM)
-        return None, dwp, dbp, dwq, dwk, dwv, None
+        return (None, None, *(dwp[i, :, :d] for i, d in enumerate(FEATURE_DIMS)),
+                *(dbp[i] for i in range(FEATURE_AMOUNT)), dwq, dwk, dwv)
+
+
+def front_params(projection, attention):
+    """Parameter order of _FusedFront.apply."""
+    return ([lin.weight for lin in projection.layers] + [lin.bias for lin in projection.layers] +
+            [attention.querys.weight, attention.keys.weight, attention.values.weight])
 
 
 class _SplitKLinear(torch.autograd.Function):
@@ -193,11 +212,7 @@ class Actor(nn.Module):
     def forward(self, x):
         x = torch.as_tensor(x, dtype=torch.float32, device=self.move_head.weight.device).reshape(-1, OBS_SPACE)
         if x.is_cuda:  # product path: fused HIP front-end (no fallback on the GPU)
-            pr = self.projection
-            wp = torch.stack([F.pad(lin.weight, (0, 4 - d)) for lin, d in zip(pr.layers, FEATURE_DIMS)])
-            bp = torch.stack([lin.bias for lin in pr.layers])
-            at = self.attention
-            h = _FusedFront.apply(x, wp, bp, at.querys.weight, at.keys.weight, at.values.weight, pr.parity_mode)
+            h = _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
         else:  # host reference path (CPU tests only)
             h = self.attention(self.projection(x))
         act = F.relu if self.activation is nn.ReLU else self.activation()

@@ -168,8 +168,7 @@ def test_train_runs_and_learns_something():
 @pytest.mark.parametrize("parity", [True, False])
 def test_fused_front_matches_torch(parity):
     """csrc/actor_front.hip forward+backward == the module-by-module torch path."""
-    from marlmaze.networks import Actor, _FusedFront, FEATURE_DIMS
-    import torch.nn.functional as F
+    from marlmaze.networks import Actor, _FusedFront, front_params
 
     torch.manual_seed(0)
     actor = Actor([264, 264, 264], parity_mode=parity).cuda()
@@ -180,12 +179,10 @@ def test_fused_front_matches_torch(parity):
     x = torch.randn(B, 65, device="cuda")
     dh = torch.randn(B, 460, device="cuda")
     pr, at = actor.projection, actor.attention
-    params = [p for m in (pr, at) for p in m.parameters()]
+    params = front_params(pr, at)
     href = at(pr(x))
     gref = torch.autograd.grad(href, params, dh)
-    wp = torch.stack([F.pad(l.weight, (0, 4 - d)) for l, d in zip(pr.layers, FEATURE_DIMS)])
-    bp = torch.stack([l.bias for l in pr.layers])
-    h = _FusedFront.apply(x, wp, bp, at.querys.weight, at.keys.weight, at.values.weight, parity)
+    h = _FusedFront.apply(x, parity, *params)
     # weights x3: large attention logits amplify summation-order differences
     np.testing.assert_allclose(h.detach().cpu().numpy(), href.detach().cpu().numpy(), rtol=1e-4, atol=2e-4)
     g = torch.autograd.grad(h, params, dh)

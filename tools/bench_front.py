@@ -6,9 +6,8 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "marl-maze_amd"))
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
 
-from marlmaze.networks import Actor, _FusedFront, FEATURE_DIMS  # noqa: E402
+from marlmaze.networks import Actor, _FusedFront, front_params  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 419430
 torch.manual_seed(0)
@@ -16,13 +15,11 @@ actor = Actor([264, 264, 264]).cuda()
 pr, at = actor.projection, actor.attention
 x = torch.rand(B, 65, device="cuda")
 dh = torch.randn(B, 460, device="cuda")
-wp = torch.stack([F.pad(l.weight, (0, 4 - d)) for l, d in zip(pr.layers, FEATURE_DIMS)]).detach().requires_grad_()
-bp = torch.stack([l.bias for l in pr.layers]).detach().requires_grad_()
-wq, wk, wv = (w.detach().requires_grad_() for w in (at.querys.weight, at.keys.weight, at.values.weight))
+params = front_params(pr, at)
 
 
 def fwd():
-    return _FusedFront.apply(x, wp, bp, wq, wk, wv, True)
+    return _FusedFront.apply(x, True, *params)
 
 
 def step():
