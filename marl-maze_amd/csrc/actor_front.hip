@@ -218,60 +218,82 @@ __global__ __launch_bounds__(256) void k_front_prep(ProjPtrs P, const float* __r
 }
 
 // ---------------------------------------------------------------------------
-// forward
+// forward (persistent: the per-token tables are staged in LDS once per workgroup)
 // ---------------------------------------------------------------------------
-constexpr int kFwdRows = 8;  // samples per 256-thread workgroup
+constexpr int kFwdRows = 8;  // samples per iteration of a 256-thread workgroup
+constexpr int kTabF = kQkv * kPin + kQkv + kEmb * kPin + kEmb;  // 300 floats per token: A | c | Wp | bp
+// (300 dwords = 75 16-byte quads, odd: a wave's per-token 16-byte reads are bank-conflict free)
+
+__device__ __forceinline__ void stage_tables(const float* __restrict__ ws, float* tab) {
+    for (int e = threadIdx.x; e < kTok * kTabF; e += blockDim.x) {
+        const int i = e / kTabF, f = e % kTabF;
+        float v;
+        if (f < kQkv * kPin) v = ws[kWsA + i * kQkv * kPin + f];
+        else if (f < kQkv * kPin + kQkv) v = ws[kWsC + i * kQkv + f - kQkv * kPin];
+        else if (f < kQkv * kPin + kQkv + kEmb * kPin) v = ws[kWsWP + i * kEmb * kPin + f - kQkv * (kPin + 1)];
+        else v = ws[kWsBP + i * kEmb + f - kQkv * (kPin + 1) - kEmb * kPin];
+        tab[e] = v;
+    }
+}
 
 __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws, const float* __restrict__ x,
                                                    int ldx, int B, int parity, float* __restrict__ h) {
+    __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
     __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKq];
     __shared__ __attribute__((aligned(16))) float Vs[kFwdRows][kTok][kEmb];
+    stage_tables(ws, tab);
     const int g = threadIdx.x >> 5;  // sample slot in the workgroup
     const int i = threadIdx.x & 31;  // token
-    const int row = blockIdx.x * kFwdRows + g;
-    const bool act = (i < kTok) && (row < B);
-    float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
-    float q[kKq];
-    if (act) {
-        xv = xslice(x + (size_t)row * ldx, i, parity != 0);
-        float o[kQkv];
-        qkv_of(ws, xv, i, o);
+    const float* ti = tab + (i < kTok ? i : 0) * kTabF;
+    const int groups = (B + kFwdRows - 1) / kFwdRows;
+    for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+        const int row = grp * kFwdRows + g;
+        const bool act = (i < kTok) && (row < B);
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (act) xv = xslice(x + (size_t)row * ldx, i, parity != 0);
+        __syncthreads();  // tables staged / previous iteration's K, V readers done
+        float q[kKq];
+        if (act) {
+            float o[kQkv];
+            affine4<kQkv>(ti, ti + kQkv * kPin, xv, o);
 #pragma unroll
-        for (int a = 0; a < kKq; a++) {
-            q[a] = o[a];
-            Ks[g][i][a] = o[kKq + a];
+            for (int a = 0; a < kKq; a++) {
+                q[a] = o[a];
+                Ks[g][i][a] = o[kKq + a];
+            }
+#pragma unroll
+            for (int c = 0; c < kEmb; c++) Vs[g][i][c] = o[2 * kKq + c];
         }
+        __syncthreads();
+        if (act) {
+            float s[kTok];
+            float mx = -INFINITY;
 #pragma unroll
-        for (int c = 0; c < kEmb; c++) Vs[g][i][c] = o[2 * kKq + c];
+            for (int j = 0; j < kTok; j++) {
+                s[j] = div_sqrt_kq(dot4<kKq>(q, Ks[g][j]));
+                mx = fmaxf(mx, s[j]);
+            }
+            float sum = 0.f;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                s[j] = expf(s[j] - mx);
+                sum += s[j];
+            }
+            float out[kEmb];
+#pragma unroll
+            for (int c = 0; c < kEmb; c++) out[c] = 0.f;
+            const float inv = 1.f / sum;  // torch's softmax scales by the reciprocal of the sum
+#pragma unroll
+            for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] * inv, Vs[g][j]);
+            float t[kEmb];
+            affine4<kEmb>(ti + kQkv * (kPin + 1), ti + kQkv * (kPin + 1) + kEmb * kPin, xv, t);
+            float* o = h + (size_t)row * kRowF + i * kEmb;
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4)
+                *reinterpret_cast<float4*>(o + c) =
+                    make_float4(t[c] + out[c], t[c + 1] + out[c + 1], t[c + 2] + out[c + 2], t[c + 3] + out[c + 3]);
+        }
     }
-    __syncthreads();
-    if (!act) return;
-    float s[kTok];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < kTok; j++) {
-        s[j] = div_sqrt_kq(dot4<kKq>(q, Ks[g][j]));
-        mx = fmaxf(mx, s[j]);
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int j = 0; j < kTok; j++) {
-        s[j] = expf(s[j] - mx);
-        sum += s[j];
-    }
-    float out[kEmb];
-#pragma unroll
-    for (int c = 0; c < kEmb; c++) out[c] = 0.f;
-    const float inv = 1.f / sum;  // torch's softmax scales by the reciprocal of the sum
-#pragma unroll
-    for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] * inv, Vs[g][j]);
-    float t[kEmb];
-    embed(ws, xv, i, t);
-    float* o = h + (size_t)row * kRowF + i * kEmb;
-#pragma unroll
-    for (int c = 0; c < kEmb; c += 4)
-        *reinterpret_cast<float4*>(o + c) =
-            make_float4(t[c] + out[c], t[c + 1] + out[c + 1], t[c + 2] + out[c + 2], t[c + 3] + out[c + 3]);
 }
 
 // ---------------------------------------------------------------------------
@@ -279,9 +301,8 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
 // ---------------------------------------------------------------------------
 // LDS per sample (floats): attention phase {K 23x10 | Q 23x10 | V 23x20 |
 // P 23x23 | dS 23x23}; after a barrier the same words hold the reduction
-// operands {G = [dq|dk|dv] 23x40 | T 23x20 | dctx 23x20 | X 23x4}.  dctx rows
-// of other tokens are re-read from global (L1/L2) in phase 3.  63 KB per
-// workgroup: two workgroups (8 waves) per CU.
+// operands {G = [dq|dk|dv] 23x40 | T 23x20 | dctx 23x20 | X 23x4}; the V rows
+// carry dctx in phase 3.  63 KB per workgroup: two workgroups (8 waves) per CU.
 constexpr int kBwdRows = 8;
 constexpr int kBwdThreads = 256;
 constexpr int kOffK = 0, kOffQ = 230, kOffV = 460, kOffP = 920, kOffS = 1449;  // attention phase
@@ -384,6 +405,13 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
                 my[kOffS + i * kTok + j] = ds;
                 axpy4<kKq>(dq, ds, my + kOffK + j * kKq);
             }
+            // v is dead once this wave's dP loop is done (a sample's 32 lanes are
+            // one wavefront, so its LDS accesses stay in program order): the V
+            // rows now carry dctx for phase 3
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4)
+                *reinterpret_cast<float4*>(my + kOffV + i * kEmb + c) =
+                    make_float4(dctx[c], dctx[c + 1], dctx[c + 2], dctx[c + 3]);
         }
         __syncthreads();
         float dk[kKq], dv[kEmb];
@@ -396,7 +424,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
             for (int j = 0; j < kTok; j++) {
                 const float pj = my[kOffP + j * kTok + i];
                 const float sj = my[kOffS + j * kTok + i];
-                const float4* cj = reinterpret_cast<const float4*>(dhr + j * kEmb);
+                const float4* cj = reinterpret_cast<const float4*>(my + kOffV + j * kEmb);
 #pragma unroll
                 for (int c = 0; c < kEmb / 4; c++) {
                     const float4 v = cj[c];
@@ -556,12 +584,22 @@ extern "C" int mm_actor_front_prep(const float* const* wproj, const float* const
     return (int)hipGetLastError();
 }
 
+static int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+    return cus[dev];
+}
+
 extern "C" int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h,
                                   void* stream) {
     if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM) return MM_E_ARG;
     if (B == 0) return 0;
-    hipLaunchKernelGGL(k_front_fwd, dim3((B + kFwdRows - 1) / kFwdRows), dim3(256), 0, (hipStream_t)stream, ws, x,
-                       ldx, B, parity, h);
+    const int groups = (B + kFwdRows - 1) / kFwdRows;
+    const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();  // three workgroups per CU
+    hipLaunchKernelGGL(k_front_fwd, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
     return (int)hipGetLastError();
 }
 
