@@ -120,6 +120,15 @@ __device__ __forceinline__ void qkv_of(const float* __restrict__ ws, float4 xv, 
     affine4<kQkv>(ws + kWsA + i * kQkv * kPin, ws + kWsC + i * kQkv, xv, o);
 }
 
+// A sample's 32 lanes are half of one wavefront, and a wavefront's LDS
+// accesses execute in program order, so hand-offs between the lanes of one
+// sample need only a compiler-level ordering point, not a workgroup barrier.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int N>
 __device__ __forceinline__ float dot4(const float* a, const float* __restrict__ b_lds) {  // N % 2 == 0
     float acc = 0.f;
@@ -242,6 +251,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
     __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKq];
     __shared__ __attribute__((aligned(16))) float Vs[kFwdRows][kTok][kEmb];
     stage_tables(ws, tab);
+    __syncthreads();
     const int g = threadIdx.x >> 5;  // sample slot in the workgroup
     const int i = threadIdx.x & 31;  // token
     const float* ti = tab + (i < kTok ? i : 0) * kTabF;
@@ -251,7 +261,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
         const bool act = (i < kTok) && (row < B);
         float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (act) xv = xslice(x + (size_t)row * ldx, i, parity != 0);
-        __syncthreads();  // tables staged / previous iteration's K, V readers done
+        wave_sync();  // previous iteration's K, V readers (this wavefront) are done
         float q[kKq];
         if (act) {
             float o[kQkv];
@@ -264,7 +274,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
 #pragma unroll
             for (int c = 0; c < kEmb; c++) Vs[g][i][c] = o[2 * kKq + c];
         }
-        __syncthreads();
+        wave_sync();
         if (act) {
             float s[kTok];
             float mx = -INFINITY;
@@ -364,7 +374,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
                 *reinterpret_cast<float4*>(my + kOffV + i * kEmb + c) =
                     make_float4(o[2 * kKq + c], o[2 * kKq + c + 1], o[2 * kKq + c + 2], o[2 * kKq + c + 3]);
         }
-        __syncthreads();
+        wave_sync();
         float dq[kKq];
         if (act) {  // phase 2: softmax row i, dP, dS, dq
             float q[kKq];
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
                 *reinterpret_cast<float4*>(my + kOffV + i * kEmb + c) =
                     make_float4(dctx[c], dctx[c + 1], dctx[c + 2], dctx[c + 3]);
         }
-        __syncthreads();
+        wave_sync();
         float dk[kKq], dv[kEmb];
         if (act) {  // phase 3: dv_i = sum_j P_ji dctx_j, dk_i = sum_j dS_ji q_j
 #pragma unroll
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
                 axpy4<kKq>(dk, sj, my + kOffQ + j * kKq);
             }
         }
-        __syncthreads();  // attention-phase words are dead: reuse them for the reduction operands
+        wave_sync();  // attention-phase words of this sample are dead: reuse them for the reduction operands
         if (act) {
             float t[kEmb];
             embed(ws, xv, i, t);
