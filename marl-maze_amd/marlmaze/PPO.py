@@ -330,30 +330,3 @@ class PPO:
             return True
         return False
 
-
-def smoke_iteration():
-    """One tiny rollout + update on cuda:0, checked against the CPU oracle's update."""
-    import oracle.ppo as oppo
-
-    agent = PPO(2, epochs=1, batch_size=1280, lr=1.4e-4, n_envs=256, horizon=5, load=False, verbose=False,
-                save=False, env_config=dict(default_size=(10, 10), max_timestep=60, seed_base=0), sample_seed=1)
-    b_obs, b_act, b_lp, _, _, b_masks, b_adv, b_val = agent.get_batch()
-    assert torch.isfinite(b_lp).all() and torch.isfinite(b_adv).all()
-    # teacher-forced comparison of one minibatch update with the oracle (CPU fp32)
-    actor, critic = oppo.OActor(), oppo.OCritic()
-    actor.load_state_dict({k: v.cpu() for k, v in agent.actor.state_dict().items()})
-    critic.load_state_dict({k: v.cpu() for k, v in agent.critic.state_dict().items()})
-    aopt = torch.optim.Adam(actor.parameters(), lr=1.4e-4)
-    copt = torch.optim.Adam(critic.parameters(), lr=1.4e-4)
-    idx = torch.arange(256)
-    adv = torch.randn(256, generator=torch.Generator().manual_seed(0))
-    rtg = torch.randn(256, generator=torch.Generator().manual_seed(1))
-    ref = oppo.minibatch_step(actor, critic, aopt, copt, b_obs[idx].cpu(), b_act[idx].cpu(), b_lp[idx].cpu(),
-                              adv, rtg, b_masks[idx].cpu())
-    got = agent.minibatch_step(b_obs[idx], b_act[idx], b_lp[idx], adv.cuda(), rtg.cuda(), b_masks[idx])
-    got = [float(x) for x in got]
-    for g, r in zip(got, ref):  # losses and gradient norms: 1e-5 relative
-        assert abs(g - r) <= 1e-5 * abs(r) + 1e-7, (got, ref)
-    # Adam's first step is lr * g/|g|: parameters move by <= lr; agree far below that
-    for k, p in actor.state_dict().items():
-        np.testing.assert_allclose(agent.actor.state_dict()[k].cpu().numpy(), p.numpy(), rtol=0, atol=2.1e-4)
