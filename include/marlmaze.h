@@ -47,7 +47,7 @@ extern "C" {
 #define MM_MASK_DIM 6
 #define MM_RNG_WORDS 625   /* CPython random.getstate()[1]: 624 words + index */
 #define MM_MAX_SIDE 41     /* layout side limit (default_size <= 21) */
-#define MM_MAZES_PER_BLOCK 64
+#define MM_MAZES_PER_BLOCK 32  /* mazes per env-step workgroup (4 lanes each) */
 
 #define MM_E_ARG (-1)
 #define MM_E_SIZE (-2)
@@ -132,6 +132,13 @@ int mm_env_reset(const mm_env_t* env, const uint8_t* reset_mask, float* obs, uin
  * or overlap the step kernel alone); = 0: nothing is reset or queued. */
 int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward, uint8_t* done,
                 int32_t* ep_stats, int auto_reset, void* stream);
+
+/* mm_env_step whose step kernel is launched with hipExtLaunchKernel: the two
+ * hipEvent_t (created by the caller with timing enabled; either may be NULL)
+ * are stamped at the step kernel's own start and end, so their elapsed time is
+ * the kernel's duration (used by bench.py for the roofline). */
+int mm_env_step_timed(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward,
+                      uint8_t* done, int32_t* ep_stats, int auto_reset, void* stream, void* ev_start, void* ev_stop);
 
 /* Maze.reset() for the mazes queued by the previous mm_env_step(auto_reset=2)
  * (writes their obs/mask rows; clears the queue). */

@@ -542,14 +542,27 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
     }
 }
 
-// sum of the partial rows (fixed order over rows: deterministic)
-__global__ __launch_bounds__(256) void k_front_sum(const float* __restrict__ partial, int rows,
-                                                   float* __restrict__ red) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= kPartLen) return;
+// sum of the partial rows: workgroup = 64 columns x 16 row classes (r mod 16);
+// each thread sums its class in row order, then the 16 class sums are added in
+// class order (fixed order: deterministic)
+constexpr int kSumCols = 64, kSumClasses = 16;
+
+__global__ __launch_bounds__(kSumCols * kSumClasses) void k_front_sum(const float* __restrict__ partial, int rows,
+                                                                      float* __restrict__ red) {
+    __shared__ float acc_s[kSumClasses][kSumCols];
+    const int c = threadIdx.x % kSumCols, k = threadIdx.x / kSumCols;
+    const int e = blockIdx.x * kSumCols + c;
     float acc = 0.f;
-    for (int r = 0; r < rows; r++) acc += partial[(size_t)r * kPartLen + e];
-    red[e] = acc;
+    if (e < kPartLen)
+        for (int r = k; r < rows; r += kSumClasses) acc += partial[(size_t)r * kPartLen + e];
+    acc_s[k][c] = acc;
+    __syncthreads();
+    if (k == 0 && e < kPartLen) {
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < kSumClasses; q++) t += acc_s[q][c];
+        red[e] = t;
+    }
 }
 
 // parameter gradients: dWqkv as summed; dWp_i = F_i + Wqkv^T E_i, dbp_i = f_i + Wqkv^T e_i
@@ -620,7 +633,8 @@ extern "C" int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int 
     hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_front_sum, dim3((kPartLen + 255) / 256), dim3(256), 0, s, partial, grid, red);
+    hipLaunchKernelGGL(k_front_sum, dim3((kPartLen + kSumCols - 1) / kSumCols), dim3(kSumCols * kSumClasses), 0, s,
+                       partial, grid, red);
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_front_combine, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, grad);

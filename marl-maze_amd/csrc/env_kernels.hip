@@ -15,6 +15,7 @@
 //            lane gathers two rays of one agent's neighbourhood as bitmasks.
 //            Finished mazes are appended to a done list that k_reset consumes
 //            (PPO.py:127-130).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,7 +27,6 @@ extern "C" int mm_layout_stride(int size_w, int size_h, int rand_sizes, int rand
 
 namespace mm {
 
-constexpr int kMPB = MM_MAZES_PER_BLOCK;  // mazes per step workgroup
 constexpr int kMaxCells = MM_MAX_SIDE * MM_MAX_SIDE;
 constexpr int kGenTries = 1 << 16;  // rejection-loop bound, same as oracle GEN_TRIES (reference: unbounded)
 constexpr int kListOff = 64;        // done list starts at work[64]
@@ -562,8 +562,9 @@ extern "C" int mm_env_reset(const mm_env_t* env, const uint8_t* reset_mask, floa
     return launch_reset(env, reset_mask, 0, obs, masks, (hipStream_t)stream);
 }
 
-extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward,
-                           uint8_t* done, int32_t* ep_stats, int auto_reset, void* stream) {
+extern "C" int mm_env_step_timed(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks,
+                                 float* reward, uint8_t* done, int32_t* ep_stats, int auto_reset, void* stream,
+                                 void* ev_start, void* ev_stop) {
     int e = check_env(env);
     if (e) return e;
     if (!actions || !obs || !masks || !reward || !done) return MM_E_ARG;
@@ -571,13 +572,19 @@ extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* ob
     hipStream_t s = (hipStream_t)stream;
     const size_t lds = step_lds_bytes(env->layout_stride);
     const int grid = (env->n + kMPB4 - 1) / kMPB4;
-    hipLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB4 * kLanes), lds, s, *env, actions, obs, masks, reward, done,
-                       ep_stats,
-                       auto_reset ? 1 : 0);
+    // hipExtLaunchKernel stamps the events at the kernel's own start / end
+    hipExtLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB4 * kLanes), (uint32_t)lds, s, (hipEvent_t)ev_start,
+                          (hipEvent_t)ev_stop, 0, *env, actions, obs, masks, reward, done, ep_stats,
+                          auto_reset ? 1 : 0);
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
     if (auto_reset == 1) return launch_reset(env, nullptr, 1, obs, masks, s);
     return 0;
+}
+
+extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward,
+                           uint8_t* done, int32_t* ep_stats, int auto_reset, void* stream) {
+    return mm_env_step_timed(env, actions, obs, masks, reward, done, ep_stats, auto_reset, stream, nullptr, nullptr);
 }
 
 extern "C" int mm_env_reset_done(const mm_env_t* env, float* obs, uint8_t* masks, void* stream) {

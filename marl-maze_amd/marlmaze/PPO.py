@@ -146,12 +146,12 @@ class PPO:
             if ev is None:
                 self.venv.step(b["act"][t], auto_reset=True, obs=b["obs"][t + 1], masks=b["masks"][t + 1],
                                reward=b["rew"][t], done=b["done"][t], ep_stats=b["stats"][t])
-            else:  # instrumented: time the env-step kernel alone (HIP events on this stream)
+            else:  # instrumented: HIP events stamped at the env-step kernel's own start / end
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                self.venv.step(b["act"][t], auto_reset=2, obs=b["obs"][t + 1], masks=b["masks"][t + 1],
-                               reward=b["rew"][t], done=b["done"][t], ep_stats=b["stats"][t])
+                e0.record()  # materialise the events; the launch re-stamps them
                 e1.record()
+                self.venv.step(b["act"][t], auto_reset=2, obs=b["obs"][t + 1], masks=b["masks"][t + 1],
+                               reward=b["rew"][t], done=b["done"][t], ep_stats=b["stats"][t], events=(e0, e1))
                 self.venv.reset_done(obs=b["obs"][t + 1], masks=b["masks"][t + 1])
                 ev.append((e0, e1))
         last = None

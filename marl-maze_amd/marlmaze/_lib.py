@@ -17,7 +17,7 @@ OBS_DIM = 65
 MASK_DIM = 6
 RNG_WORDS = 625
 MAX_SIDE = 41
-MAZES_PER_BLOCK = 64
+MAZES_PER_BLOCK = 32
 
 ST_GEN_FAIL = 1
 ST_BAD_MOVE = 2
@@ -32,7 +32,7 @@ AF_HAS_MARK = 64
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
-           "mm_env_step", "mm_env_reset_done", "mm_gae", "mm_sample",
+           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_gae", "mm_sample",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd")
 
@@ -76,6 +76,8 @@ def lib():
         L.mm_env_reset.restype = i32
         L.mm_env_step.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P, P, P, i32, P]
         L.mm_env_step.restype = i32
+        L.mm_env_step_timed.argtypes = [ctypes.POINTER(EnvDesc), P, P, P, P, P, P, i32, P, P, P]
+        L.mm_env_step_timed.restype = i32
         L.mm_env_reset_done.argtypes = [ctypes.POINTER(EnvDesc), P, P, P]
         L.mm_env_reset_done.restype = i32
         L.mm_gae.argtypes = [P, P, P, P, i32, i32, f32, f32, P, P, P]

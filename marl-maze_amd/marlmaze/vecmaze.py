@@ -104,7 +104,8 @@ class VecMaze:
                                            _lib.ptr(masks), _lib.stream_ptr()), "mm_env_reset")
         return obs, masks
 
-    def step(self, actions, auto_reset=True, obs=None, masks=None, reward=None, done=None, ep_stats=None):
+    def step(self, actions, auto_reset=True, obs=None, masks=None, reward=None, done=None, ep_stats=None,
+             events=None):
         """Maze.step(actions) for all mazes (maze.py:74-122).
 
         actions: [n, 2, 2] int8 (move 0..4, mark 0/1) on the device.  With
@@ -113,6 +114,9 @@ class VecMaze:
         ``auto_reset=2`` only queues them for ``reset_done()``.
         ep_stats: optional [n, 2] int32 receiving (episode length, shortest
         path length) for the mazes that finished this step.
+        events: optional (start, end) ``torch.cuda.Event`` pair (timing
+        enabled, already recorded once) stamped at the step kernel's own start
+        and end (mm_env_step_timed).
         """
         obs = self.obs if obs is None else obs
         masks = self.masks if masks is None else masks
@@ -120,9 +124,16 @@ class VecMaze:
         done = self.done if done is None else done
         if actions.dtype != torch.int8 or not actions.is_contiguous():
             actions = actions.to(torch.int8).contiguous()
-        _lib.check(_lib.lib().mm_env_step(ctypes.byref(self._desc), _lib.ptr(actions), _lib.ptr(obs),
-                                          _lib.ptr(masks), _lib.ptr(reward), _lib.ptr(done), _lib.ptr(ep_stats),
-                                          int(auto_reset), _lib.stream_ptr()), "mm_env_step")
+        if events is None:
+            _lib.check(_lib.lib().mm_env_step(ctypes.byref(self._desc), _lib.ptr(actions), _lib.ptr(obs),
+                                              _lib.ptr(masks), _lib.ptr(reward), _lib.ptr(done), _lib.ptr(ep_stats),
+                                              int(auto_reset), _lib.stream_ptr()), "mm_env_step")
+        else:
+            e0, e1 = (ctypes.c_void_p(e.cuda_event) if e is not None else None for e in events)
+            _lib.check(_lib.lib().mm_env_step_timed(ctypes.byref(self._desc), _lib.ptr(actions), _lib.ptr(obs),
+                                                    _lib.ptr(masks), _lib.ptr(reward), _lib.ptr(done),
+                                                    _lib.ptr(ep_stats), int(auto_reset), _lib.stream_ptr(), e0, e1),
+                       "mm_env_step_timed")
         return obs, masks, reward, done
 
     def reset_done(self, obs=None, masks=None):
