@@ -60,8 +60,10 @@ class PPO:
         self.critic = Critic(agent_amount, hidden_sizes=[64, 64]).to(self.device)
         torch.random.set_rng_state(g)
         self.dp.broadcast_params([self.actor, self.critic])
-        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=lr)
-        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=lr)
+        # Adam (PPO.py:18-19); on the GPU the fused multi-tensor kernel (same update rule, one launch)
+        fused = self.device.type == "cuda"
+        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=lr, fused=fused)
+        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=lr, fused=fused)
 
         self.agent_amount = agent_amount
         self.epochs = epochs
@@ -208,8 +210,8 @@ class PPO:
         s2 = torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv
         actor_loss = -torch.mean(torch.min(s1, s2))
         critic_loss = torch.nn.functional.mse_loss(V, rtg)
-        self.actor_optim.zero_grad(set_to_none=False)
-        self.critic_optim.zero_grad(set_to_none=False)
+        self.actor_optim.zero_grad(set_to_none=True)  # backward assigns fresh gradients: no fill + add launches
+        self.critic_optim.zero_grad(set_to_none=True)
         (actor_loss + critic_loss).backward()  # disjoint parameters: same grads as two backwards
         params = list(self.actor.parameters()) + list(self.critic.parameters())
         self.dp.allreduce_grads(params)
@@ -314,9 +316,20 @@ class PPO:
                 group["lr"] *= 0.997
 
     def save_parameters(self):
-        torch.save({"actor": self.actor.state_dict(), "critic": self.critic.state_dict(),
-                    "actor_optim": self.actor_optim.state_dict(),
-                    "critic_optim": self.critic_optim.state_dict()}, self.model_path)
+        """PPO.py:222-230: the same four entries; tensors are saved on the CPU so
+        the reference (CPU torch) can load the file as it loads its own."""
+        def cpu(o):
+            if torch.is_tensor(o):
+                return o.detach().cpu()
+            if isinstance(o, dict):
+                return {k: cpu(v) for k, v in o.items()}
+            if isinstance(o, (list, tuple)):
+                return type(o)(cpu(v) for v in o)
+            return o
+
+        torch.save(cpu({"actor": self.actor.state_dict(), "critic": self.critic.state_dict(),
+                        "actor_optim": self.actor_optim.state_dict(),
+                        "critic_optim": self.critic_optim.state_dict()}), self.model_path)
 
     def load_parameters(self):
         if os.path.exists(self.model_path):

@@ -68,10 +68,10 @@ class DP:
         torch.cat([g.reshape(-1) for g in grads], out=flat)
         dist.all_reduce(flat, op=dist.ReduceOp.SUM)
         flat.mul_(1.0 / self.world)
-        off = 0
-        for g in grads:
+        off = 0  # the averaged gradients ARE the bucket: each .grad becomes a view of it (no copy back)
+        for p, g in zip(params, grads):
             k = g.numel()
-            g.copy_(flat[off:off + k].view_as(g))
+            p.grad = flat[off:off + k].view_as(g)
             off += k
 
     def global_mean_std(self, x):

@@ -151,21 +151,35 @@ def front_params(projection, attention):
             [attention.querys.weight, attention.keys.weight, attention.values.weight])
 
 
+def _linear_fwd(x, w, b, relu):
+    """y = x W^T + b (then ReLU), the ReLU in the GEMM epilogue on the GPU."""
+    if relu and x.is_cuda and x.dim() == 2:
+        return torch._addmm_activation(b, x, w.t())
+    y = F.linear(x, w, b)
+    return F.relu(y) if relu else y
+
+
 class _SplitKLinear(torch.autograd.Function):
-    """nn.Linear whose weight gradient dW = dY^T X (a reduction over all
-    M >> 10^5 rows into a 264 x 460 tile grid) runs as a split-K batched GEMM:
-    S slices of M/S rows each, then a sum over the S partial [out, in] tiles.
-    As one GEMM the reduction gets only (out/32)*(in/32) output tiles, far
-    fewer than the 256 CUs; split S ways it fills the chip."""
+    """nn.Linear (optionally followed by ReLU) whose weight gradient dW = dY^T X
+    (a reduction over all M >> 10^5 rows into a 264 x 460 tile grid) runs as
+    a split-K batched GEMM: S slices of M/S rows each, then a sum over the S
+    partial [out, in] tiles.  As one GEMM the reduction gets only
+    (out/32)*(in/32) output tiles, far fewer than the 256 CUs; split S ways it
+    fills the chip.  With relu=True the forward GEMM applies bias + ReLU in
+    its epilogue and the backward masks dY by y > 0 (threshold_backward)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
-        return F.linear(x, w, b)
+    def forward(ctx, x, w, b, relu):
+        y = _linear_fwd(x, w, b, relu)
+        ctx.relu = relu
+        ctx.save_for_backward(x, w, y if relu else None)
+        return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        x, w, y = ctx.saved_tensors
+        if ctx.relu:
+            dy = torch.ops.aten.threshold_backward(dy, y, 0)
         dx = dy.mm(w)
         M = x.shape[0]
         S = 16 if M >= 16 * 4096 else 1
@@ -176,13 +190,13 @@ class _SplitKLinear(torch.autograd.Function):
                 dw = dw + dy[m:].t().mm(x[m:])
         else:
             dw = dy.t().mm(x)
-        return dx, dw, dy.sum(0)
+        return dx, dw, dy.sum(0), None
 
 
-def _linear(x, w, b):
+def _linear(x, w, b, relu=False):
     if x.is_cuda and torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
-        return _SplitKLinear.apply(x, w, b)
-    return F.linear(x, w, b)
+        return _SplitKLinear.apply(x, w, b, relu)
+    return _linear_fwd(x, w, b, relu)
 
 
 class Actor(nn.Module):
@@ -215,9 +229,13 @@ class Actor(nn.Module):
             h = _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
         else:  # host reference path (CPU tests only)
             h = self.attention(self.projection(x))
-        act = F.relu if self.activation is nn.ReLU else self.activation()
-        for lin in self.layers:
-            h = act(_linear(h, lin.weight, lin.bias))
+        if self.activation is nn.ReLU:
+            for lin in self.layers:
+                h = _linear(h, lin.weight, lin.bias, relu=True)
+        else:
+            act = self.activation()
+            for lin in self.layers:
+                h = act(_linear(h, lin.weight, lin.bias))
         heads = _linear(h, torch.cat([self.move_head.weight, self.mark_head.weight], 0),
                         torch.cat([self.move_head.bias, self.mark_head.bias], 0))
         return [heads[:, :5], heads[:, 5:6]]
@@ -245,7 +263,9 @@ class Critic(nn.Module):
     def forward(self, x):
         x = torch.as_tensor(x, dtype=torch.float32, device=self.layers[0].weight.device)
         x = x.reshape(-1, self.agent_amount * OBS_SPACE)
-        act = F.relu if self.activation is nn.ReLU else self.activation()
         for lin in self.layers[:-1]:
-            x = act(_linear(x, lin.weight, lin.bias))
+            if self.activation is nn.ReLU:
+                x = _linear(x, lin.weight, lin.bias, relu=True)
+            else:
+                x = self.activation()(_linear(x, lin.weight, lin.bias))
         return _linear(x, self.layers[-1].weight, self.layers[-1].bias)

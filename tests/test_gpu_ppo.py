@@ -188,3 +188,43 @@ def test_fused_front_matches_torch(parity):
     g = torch.autograd.grad(h, params, dh)
     for a, b in zip(g, gref):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-3 * b.abs().max().item())
+
+
+def test_checkpoint_round_trip_reference_format(tmp_path, golden):
+    """F1 (PPO.py:222-238): a checkpoint written the reference's way (CPU
+    torch Actor/Critic + Adam state dicts) loads into the GPU PPO, training
+    continues from its Adam state, and the GPU PPO's own checkpoint loads back
+    on the CPU with weights_only=True into the reference-shaped modules."""
+    c = golden("ckpt_logits")
+    actor, critic = oppo.OActor(), oppo.OCritic()
+    actor.load_state_dict({k[6:]: torch.as_tensor(c[k]) for k in c.files if k.startswith("actor/")})
+    critic.load_state_dict({k[7:]: torch.as_tensor(c[k]) for k in c.files if k.startswith("critic/")})
+    aopt = torch.optim.Adam(actor.parameters(), lr=1.4e-4)
+    copt = torch.optim.Adam(critic.parameters(), lr=1.4e-4)
+    for opt, m in ((aopt, actor), (copt, critic)):  # give Adam a state, as a trained reference run has
+        opt.zero_grad()
+        sum(p.sum() for p in m.parameters()).backward()
+        opt.step()
+    ref_path = str(tmp_path / "PPO.pth")
+    torch.save({"actor": actor.state_dict(), "critic": critic.state_dict(), "actor_optim": aopt.state_dict(),
+                "critic_optim": copt.state_dict()}, ref_path)
+    ag = PPO(2, n_envs=64, load=True, model_path=ref_path, verbose=False, save=False)
+    for k, v in actor.state_dict().items():
+        assert torch.equal(ag.actor.state_dict()[k].cpu(), v), k
+    st = ag.actor_optim.state_dict()["state"]
+    assert float(st[0]["step"]) == 1.0 and torch.equal(st[0]["exp_avg"].cpu(), aopt.state_dict()["state"][0]["exp_avg"])
+    o = torch.as_tensor(c["obs"]).cuda()
+    with torch.no_grad():
+        mv, _ = ag.actor(o.reshape(-1, 65))
+    mv_ref, _ = actor(o.reshape(-1, 65).cpu())
+    np.testing.assert_allclose(mv.cpu().numpy(), mv_ref.detach().numpy(), rtol=RTOL, atol=1e-5)
+    # the GPU side writes a CPU-loadable checkpoint with the reference keys
+    ag.model_path = str(tmp_path / "PPO_gpu.pth")
+    ag.save_parameters()
+    sd = torch.load(ag.model_path, weights_only=True)
+    assert set(sd) == {"actor", "critic", "actor_optim", "critic_optim"}
+    actor2 = oppo.OActor()
+    actor2.load_state_dict(sd["actor"])
+    aopt2 = torch.optim.Adam(actor2.parameters(), lr=1.4e-4)
+    aopt2.load_state_dict(sd["actor_optim"])
+    assert all(not t.is_cuda for t in sd["actor"].values())
