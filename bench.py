@@ -80,9 +80,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     a = ap.parse_args()
 
-    dp = DP.from_env()
+    # MARLMAZE_DP_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
+    # the default is nccl (= RCCL) with one rank per GPU
+    dp = DP.from_env(backend=os.environ.get("MARLMAZE_DP_BACKEND"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     world = dp.world
     if world != a.gpus and dp.rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
