@@ -233,13 +233,19 @@ class PPO:
             index_list = torch.as_tensor(index_list, device=b_obs.device, dtype=torch.long)
         local_bs = min(self.batch_size // self.dp.world, B) if self.dp.active else self.batch_size
         mb = local_bs // 5 if self.dp.active else self.mbatch_size
+        # the reference shuffles once per batch (PPO.py:48-49): gather the batch into that order once,
+        # so every minibatch is a contiguous slice (same rows, no per-minibatch gathers)
+        used = min(B, ((local_bs + mb - 1) // mb) * mb)
+        order = index_list[:used]
+        p_obs, p_act, p_logp, p_advs, p_rtgs, p_masks = (t[order] for t in (b_obs, b_act, b_logp, b_advs, b_rtgs,
+                                                                          b_masks))
         hist = []
         for _ in range(self.updates_per_batch):
             self.decay_lr()
             for start in range(0, local_bs, mb):
-                idx = index_list[start:start + mb]
-                hist.append(torch.stack(self.minibatch_step(b_obs[idx], b_act[idx], b_logp[idx], b_advs[idx],
-                                                            b_rtgs[idx], b_masks[idx])))
+                sl = slice(start, start + mb)
+                hist.append(torch.stack(self.minibatch_step(p_obs[sl], p_act[sl], p_logp[sl], p_advs[sl],
+                                                            p_rtgs[sl], p_masks[sl])))
         hist = torch.stack(hist)
         if self.dp.active:  # local losses -> global-minibatch losses (equal shards); norms are already global
             self.dp.allreduce_sum(hist)
