@@ -164,6 +164,16 @@ int mm_gae(const float* reward, const float* value, const uint8_t* done, const f
 int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M, uint64_t seed,
               uint64_t offset, int8_t* actions, float* logp, float* joint_logp, void* stream);
 
+/* The actor's two heads fused with mm_sample: logits =
+ * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]
+ * [6, K] and b [6] (networks.py:38-41), then the draw of mm_sample with the
+ * same Philox counters (seed, offset, row).  h [M, ldh] f32 is the last hidden
+ * layer (K % 4 == 0, K <= 1024, 16-byte aligned rows).  logits [M, 6] may be
+ * NULL (it receives the 5 move logits and the mark logit when given). */
+int mm_head_sample(const float* h, int ldh, int K, const float* w, const float* b, const uint8_t* masks, int M,
+                   uint64_t seed, uint64_t offset, int8_t* actions, float* logp, float* joint_logp, float* logits,
+                   void* stream);
+
 /* Actor front-end, fused (networks.py:31-34,51-82): the 23 feature embeddings
  * (Projection; parity != 0 keeps quirk Q1, every embedding reads x[:, 0:d_i]),
  * Q/K/V, softmax(QK^T/sqrt(10))V and the residual.

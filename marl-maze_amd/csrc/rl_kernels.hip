@@ -11,6 +11,8 @@
 //   k_sample  PPO.get_action (PPO.py:170-186) for every agent row: masked
 //             categorical move + Bernoulli mark, per-agent and joint log-prob,
 //             counter-based Philox4x32-10 draws.
+//   k_head_sample  the actor's two heads (networks.py:38-41) fused with
+//             k_sample's draw: last hidden layer -> actions, log-probs.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -72,6 +74,59 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
 
 __device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 
+// One agent row of PPO.get_action (PPO.py:170-186): masked categorical move,
+// Bernoulli mark; returns the per-agent log-prob.  The draws are Philox of
+// counter (offset, row): the same row gets the same numbers in k_sample and
+// k_head_sample.
+__device__ __forceinline__ float sample_row(const float ml[5], float kl, const uint8_t* __restrict__ mk, int row,
+                                            uint64_t seed, uint64_t offset, int& move, int& mark) {
+    const uint4 rnd = philox(make_uint4((uint32_t)offset, (uint32_t)(offset >> 32), (uint32_t)row, 0u),
+                             make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+    float l[5];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        l[j] = mk[j] ? ml[j] : -INFINITY;  // masked_fill(~mask, -inf)
+        mx = fmaxf(mx, l[j]);
+    }
+    float p[5], sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        p[j] = mk[j] ? expf(l[j] - mx) : 0.f;
+        sum += p[j];
+    }
+    // inverse-CDF draw over the allowed moves
+    const float target = u01(rnd.x) * sum;
+    int mv = -1, last = -1;
+    float c = 0.f;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        if (!mk[j]) continue;
+        last = j;
+        c += p[j];
+        if (mv < 0 && target < c) mv = j;
+    }
+    if (mv < 0) mv = last;
+    float lp;
+    if (mv < 0) {  // no legal move: the reference's Categorical is undefined (NaN)
+        mv = 4;
+        lp = NAN;
+    } else {
+        lp = (l[mv] - mx) - logf(sum);  // Categorical.log_prob = logit - logsumexp
+    }
+    // mark ~ Bernoulli(sigmoid(mark_logit)) if allowed else 0 (PPO.py:179-181)
+    int mk5 = 0;
+    float pm = 0.f;
+    if (mk[5]) {
+        pm = 1.f / (1.f + expf(-kl));
+        mk5 = u01(rnd.y) < pm ? 1 : 0;
+    }
+    lp += logf(mk5 ? pm : 1.f - pm);
+    move = mv;
+    mark = mk5;
+    return lp;
+}
+
 // One thread per maze: rows 2i (agent 0) and 2i+1 (agent 1).
 __global__ void k_sample(const float* __restrict__ ml, const float* __restrict__ kl, const uint8_t* __restrict__ masks,
                          int M, uint64_t seed, uint64_t offset, int8_t* __restrict__ act, float* __restrict__ logp,
@@ -84,55 +139,85 @@ __global__ void k_sample(const float* __restrict__ ml, const float* __restrict__
     for (int a = 0; a < 2; a++) {
         const int row = 2 * i + a;
         if (row >= M) break;
-        const uint4 rnd = philox(make_uint4((uint32_t)offset, (uint32_t)(offset >> 32), (uint32_t)row, 0u),
-                                 make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
-        const uint8_t* mk = masks + (size_t)row * MM_MASK_DIM;
         float l[5];
-        float mx = -INFINITY;
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
-            l[j] = mk[j] ? ml[(size_t)row * 5 + j] : -INFINITY;  // masked_fill(~mask, -inf)
-            mx = fmaxf(mx, l[j]);
-        }
-        float p[5], sum = 0.f;
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            p[j] = mk[j] ? expf(l[j] - mx) : 0.f;
-            sum += p[j];
-        }
-        // inverse-CDF draw over the allowed moves
-        const float target = u01(rnd.x) * sum;
-        int move = -1, last = -1;
-        float c = 0.f;
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            if (!mk[j]) continue;
-            last = j;
-            c += p[j];
-            if (move < 0 && target < c) move = j;
-        }
-        if (move < 0) move = last;
-        float lp;
-        if (move < 0) {  // no legal move: the reference's Categorical is undefined (NaN)
-            move = 4;
-            lp = NAN;
-        } else {
-            lp = (l[move] - mx) - logf(sum);  // Categorical.log_prob = logit - logsumexp
-        }
-        // mark ~ Bernoulli(sigmoid(mark_logit)) if allowed else 0 (PPO.py:179-181)
-        int mark = 0;
-        float pm = 0.f;
-        if (mk[5]) {
-            pm = 1.f / (1.f + expf(-kl[row]));
-            mark = u01(rnd.y) < pm ? 1 : 0;
-        }
-        lp += logf(mark ? pm : 1.f - pm);
+        for (int j = 0; j < 5; j++) l[j] = ml[(size_t)row * 5 + j];
+        int move, mark;
+        const float lp = sample_row(l, kl[row], masks + (size_t)row * MM_MASK_DIM, row, seed, offset, move, mark);
         act[2 * row] = (int8_t)move;
         act[2 * row + 1] = (int8_t)mark;
         if (logp) logp[row] = lp;
         jl += lp;
     }
     if (joint) joint[i] = jl;
+}
+
+// ---------------------------------------------------------------------------
+// fused policy head + sampler
+// ---------------------------------------------------------------------------
+// logits = h W^T + b for the concatenated heads W = [move_head; mark_head]
+// [6, K] (networks.py:38-41), then sample_row -- the logits never leave the
+// registers.  8 lanes per row (each lane a 4-column stride of the row, so a
+// row's 8 lanes read 128 contiguous bytes per step), 32 rows = 16 mazes per
+// 256-thread workgroup; head weights staged in LDS.
+constexpr int kHsLanes = 8;
+constexpr int kHsRows = 32;
+constexpr int kHsMaxK = 1024;
+
+__global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* __restrict__ h, int ldh, int K,
+                                                                   const float* __restrict__ w,
+                                                                   const float* __restrict__ b,
+                                                                   const uint8_t* __restrict__ masks, int M,
+                                                                   uint64_t seed, uint64_t offset,
+                                                                   int8_t* __restrict__ act, float* __restrict__ logp,
+                                                                   float* __restrict__ joint,
+                                                                   float* __restrict__ logits) {
+    __shared__ __attribute__((aligned(16))) float W[6 * kHsMaxK];
+    for (int e = threadIdx.x; e < 6 * K; e += blockDim.x) W[e] = w[e];
+    __syncthreads();
+    const int j = threadIdx.x % kHsLanes;
+    const int row = blockIdx.x * kHsRows + threadIdx.x / kHsLanes;
+    const bool valid = row < M;
+    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (valid) {
+        const float* hr = h + (size_t)row * ldh;
+        for (int c = 4 * j; c < K; c += 4 * kHsLanes) {
+            const float4 hv = *reinterpret_cast<const float4*>(hr + c);
+#pragma unroll
+            for (int o = 0; o < 6; o++) {
+                const float4 wv = *reinterpret_cast<const float4*>(W + o * K + c);
+                acc[o] = fmaf(hv.x, wv.x, acc[o]);
+                acc[o] = fmaf(hv.y, wv.y, acc[o]);
+                acc[o] = fmaf(hv.z, wv.z, acc[o]);
+                acc[o] = fmaf(hv.w, wv.w, acc[o]);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < 6; o++) {  // butterfly over the row's 8 lanes: every lane holds the sums
+#pragma unroll
+        for (int d = kHsLanes / 2; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+    }
+    float lp = 0.f;
+    if (valid && j == 0) {
+        float l[5];
+#pragma unroll
+        for (int o = 0; o < 5; o++) l[o] = acc[o] + b[o];
+        const float kl = acc[5] + b[5];
+        int move, mark;
+        lp = sample_row(l, kl, masks + (size_t)row * MM_MASK_DIM, row, seed, offset, move, mark);
+        act[2 * row] = (int8_t)move;
+        act[2 * row + 1] = (int8_t)mark;
+        if (logp) logp[row] = lp;
+        if (logits) {
+#pragma unroll
+            for (int o = 0; o < 5; o++) logits[(size_t)row * 6 + o] = l[o];
+            logits[(size_t)row * 6 + 5] = kl;
+        }
+    }
+    // joint log-prob of maze row/2: rows 2i and 2i+1 are adjacent 8-lane groups
+    const float other = __shfl_down(lp, kHsLanes);
+    if (joint && valid && j == 0 && (row & 1) == 0) joint[row >> 1] = lp + (row + 1 < M ? other : 0.f);
 }
 
 }  // namespace mm
@@ -156,5 +241,18 @@ extern "C" int mm_sample(const float* move_logits, const float* mark_logits, con
     const int nm = (M + 1) / 2;
     hipLaunchKernelGGL(k_sample, dim3((nm + 255) / 256), dim3(256), 0, (hipStream_t)stream, move_logits, mark_logits,
                        masks, M, seed, offset, actions, logp, joint_logp);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_head_sample(const float* h, int ldh, int K, const float* w, const float* b, const uint8_t* masks,
+                              int M, uint64_t seed, uint64_t offset, int8_t* actions, float* logp, float* joint_logp,
+                              float* logits, void* stream) {
+    if (!h || !w || !b || !masks || !actions || M < 0 || K <= 0 || (K & 3) || K > kHsMaxK || ldh < K || (ldh & 3) ||
+        ((uintptr_t)h & 15))
+        return MM_E_ARG;
+    if (M == 0) return 0;
+    hipLaunchKernelGGL(k_head_sample, dim3((M + kHsRows - 1) / kHsRows), dim3(kHsLanes * kHsRows), 0,
+                       (hipStream_t)stream, h, ldh, K, w, b, masks, M, seed, offset, actions, logp, joint_logp,
+                       logits);
     return (int)hipGetLastError();
 }

@@ -137,12 +137,14 @@ class PPO:
         """Advance every maze ``horizon`` steps; fills the [T, N] buffers."""
         self._ensure_env()
         b, n, T = self._bufs, self.n_envs, self.horizon
+        head_w, head_b = self.actor.heads()
         for t in range(T):
             obs_t = b["obs"][t]
             b["val"][t] = self.critic(obs_t).view(n)
-            ml, kl = self.actor(obs_t.view(2 * n, 65))
-            ops.sample(ml, kl, b["masks"][t].view(2 * n, 6), self.sample_seed, self._sample_offset,
-                       actions=b["act"][t].view(2 * n, 2), logp=b["rowlogp"][t], joint_logp=b["logp"][t])
+            # actor trunk, then heads + sampling fused (PPO.py:170-186; ops.head_sample)
+            h = self.actor.trunk(obs_t.view(2 * n, 65))
+            ops.head_sample(h, head_w, head_b, b["masks"][t].view(2 * n, 6), self.sample_seed, self._sample_offset,
+                            actions=b["act"][t].view(2 * n, 2), logp=b["rowlogp"][t], joint_logp=b["logp"][t])
             self._sample_offset += 1
             ev = self.step_events
             if ev is None:

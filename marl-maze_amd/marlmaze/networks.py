@@ -223,7 +223,19 @@ class Actor(nn.Module):
             self.move_head.weight *= 0.01
             self.mark_head.weight *= 0.01
 
+    def heads(self):
+        """[move_head; mark_head] as one [6, K] weight and [6] bias."""
+        return (torch.cat([self.move_head.weight, self.mark_head.weight], 0),
+                torch.cat([self.move_head.bias, self.mark_head.bias], 0))
+
     def forward(self, x):
+        h = self.trunk(x)
+        w, b = self.heads()
+        heads = _linear(h, w, b)
+        return [heads[:, :5], heads[:, 5:6]]
+
+    def trunk(self, x):
+        """Everything up to the last hidden layer (networks.py:31-36)."""
         x = torch.as_tensor(x, dtype=torch.float32, device=self.move_head.weight.device).reshape(-1, OBS_SPACE)
         if x.is_cuda:  # product path: fused HIP front-end (no fallback on the GPU)
             h = _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
@@ -236,9 +248,7 @@ class Actor(nn.Module):
             act = self.activation()
             for lin in self.layers:
                 h = act(_linear(h, lin.weight, lin.bias))
-        heads = _linear(h, torch.cat([self.move_head.weight, self.mark_head.weight], 0),
-                        torch.cat([self.move_head.bias, self.mark_head.bias], 0))
-        return [heads[:, :5], heads[:, 5:6]]
+        return h
 
 
 class Critic(nn.Module):

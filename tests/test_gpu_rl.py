@@ -116,3 +116,36 @@ def test_sampler_distribution():
     assert np.abs(freq - p).max() < 4 * np.sqrt(p.max() / M) + 1e-4
     pm = 1 / (1 + np.exp(-0.7))
     assert abs(a[:, 1].mean() - pm) < 4 * np.sqrt(pm * (1 - pm) / M)
+
+
+def test_head_sample_matches_unfused_path():
+    """F3: heads GEMM + sampler fused == actor heads (torch) then mm_sample on
+    the same Philox counters: logits at fp32 tolerance, the same draws."""
+    from marlmaze.networks import Actor
+
+    torch.manual_seed(1)
+    actor = Actor([264, 264, 264]).cuda()
+    with torch.no_grad():  # larger head weights than the 0.01 init so the draws are not trivially uniform
+        actor.move_head.weight.mul_(100.0)
+        actor.mark_head.weight.mul_(100.0)
+    M = 40001
+    x = torch.rand(M, 65, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(2)
+    masks = (torch.rand(M, 6, device="cuda", generator=g) < 0.7).to(torch.uint8)
+    with torch.no_grad():
+        h = actor.trunk(x)
+        w, b = actor.heads()
+        ml, kl = actor(x)
+        a0, lp0, j0 = ops.sample(ml, kl.view(-1), masks, seed=7, offset=3)
+        logits = torch.empty(M, 6, device="cuda")
+        a1, lp1, j1 = ops.head_sample(h, w, b, masks, seed=7, offset=3, logits=logits)
+    torch.testing.assert_close(logits[:, :5], ml, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(logits[:, 5], kl.view(-1), rtol=1e-5, atol=1e-5)
+    same = (a0 == a1).all(1)
+    assert same.float().mean().item() > 0.999  # a draw can flip only where a logit difference lands on the CDF
+    fin = same & torch.isfinite(lp0)
+    torch.testing.assert_close(lp1[fin], lp0[fin], rtol=1e-5, atol=1e-5)
+    legal = masks[torch.arange(M, device="cuda"), a1[:, 0].long()].bool() | (masks[:, :5].sum(1) == 0)
+    assert legal.all()
+    jr = lp1.view(-1)[: M - 1:2] + lp1.view(-1)[1:M:2]
+    torch.testing.assert_close(j1[: (M - 1) // 2 + 0][: jr.numel()], jr, rtol=0, atol=0, equal_nan=True)
