@@ -164,6 +164,17 @@ int mm_gae(const float* reward, const float* value, const uint8_t* done, const f
 int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M, uint64_t seed,
               uint64_t offset, int8_t* actions, float* logp, float* joint_logp, void* stream);
 
+/* C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (ReLU if relu != 0), fp32 in and
+ * out (row-major, K contiguous, K % 4 == 0, A and B 16-byte aligned), computed
+ * on the bf16 MFMA with each operand split exactly into three bf16 parts and
+ * the six partial products >= 2^-16 |a b| accumulated in fp32 (csrc/gemm_x3.hip):
+ * fp32-class accuracy at 417 TFLOP/s of peak instead of the f32 MFMA's 157.
+ * nn.Linear forward: A = x, B = weight.  Input gradient: A = dY, B = weight^T. */
+int mm_gemm_x3(const float* A, const float* B, const float* bias, float* C, int M, int N, int K, int relu,
+               uint16_t* bsplit, void* stream);
+/* uint16 elements of the bsplit scratch mm_gemm_x3 needs for B [N, K]. */
+int mm_gemm_x3_bsplit_len(int N, int K);
+
 /* The actor's two heads fused with mm_sample: logits =
  * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]
  * [6, K] and b [6] (networks.py:38-41), then the draw of mm_sample with the

@@ -1,0 +1,227 @@
+// gemm_x3.hip -- fp32 GEMMs of the actor/critic MLP on gfx950's bf16 MFMA.
+//
+// gfx950 runs f32-input MFMA at 1/16 of the bf16 MFMA rate (157 vs 2,500
+// TFLOP/s dense).  Each fp32 operand is split exactly into three bf16 parts,
+// x = hi + mid + lo (hi = RN_bf16(x), mid = RN_bf16(x - hi), lo =
+// RN_bf16(x - hi - mid); the subtractions are exact in fp32, and the three
+// parts carry all 24 significand bits).  A product a*b is then the sum of nine
+// bf16 products, each exact in the fp32 accumulator; the six whose magnitude
+// is >= 2^-16 |a b| are kept (hi*hi, hi*mid, mid*hi, mid*mid, hi*lo, lo*hi),
+// the dropped three are below 2^-23 |a b|, i.e. at the level of one fp32
+// rounding.  Accumulation is fp32 (MFMA accumulators), as in an fp32 GEMM.
+// Six bf16 MFMAs per fp32 product: 2,500 / 6 = 417 TFLOP/s of fp32-accurate
+// peak against 157 for the f32 MFMA.
+//
+// Kernel: C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (ReLU), all row-major fp32
+// with K contiguous -- the layout of y = x W^T (nn.Linear forward) and, with
+// B = W^T, of dX = dY W.  Workgroup = 8 waves, tile 256 rows x 16*NT
+// columns, K in steps of 32 (one mfma_f32_16x16x32_bf16 k-step).  The fp32
+// tiles are loaded, split and written to LDS as three bf16 planes; each wave
+// owns 32 rows x 16*NT columns (2 x NT accumulator tiles).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "marlmaze.h"
+
+namespace mm {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int kGBM = 256;      // rows per workgroup
+constexpr int kGBK = 32;       // k per step
+constexpr int kGWaves = 8;
+constexpr int kGThreads = kGWaves * 64;
+constexpr int kGLd = kGBK + 8;  // bf16 per LDS row (80 B: 16-B reads of a 16-row fragment hit distinct banks)
+
+__device__ __forceinline__ uint32_t bf16_rn(float x) {  // round-to-nearest-even, finite x
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+// x -> (hi, mid, lo) bf16 bit patterns
+__device__ __forceinline__ void split3(float x, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+    hi = bf16_rn(x);
+    const float r1 = x - __uint_as_float(hi << 16);
+    mid = bf16_rn(r1);
+    const float r2 = r1 - __uint_as_float(mid << 16);
+    lo = bf16_rn(r2);
+}
+
+// (unused by the pipelined kernel; kept for reference of the plane layout)
+// Stage rows [r0, r0 + rows) x k [k0, k0 + 32) of an fp32 [R, K] matrix into
+// three bf16 planes [rows][kGLd]; out-of-range rows / k are zero.
+__device__ __forceinline__ void stage_split(const float* __restrict__ src, int R, int K, int r0, int k0, int rows,
+                                            uint16_t* __restrict__ p_hi, uint16_t* __restrict__ p_mid,
+                                            uint16_t* __restrict__ p_lo) {
+    const int quads = rows * (kGBK / 4);
+    for (int e = threadIdx.x; e < quads; e += kGThreads) {
+        const int r = e / (kGBK / 4), kq = e % (kGBK / 4);
+        const int gr = r0 + r, gk = k0 + 4 * kq;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gr < R && gk < K) v = *reinterpret_cast<const float4*>(src + (size_t)gr * K + gk);
+        uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+        split3(v.x, h0, m0, l0);
+        split3(v.y, h1, m1, l1);
+        split3(v.z, h2, m2, l2);
+        split3(v.w, h3, m3, l3);
+        const int o = r * kGLd + 4 * kq;
+        *reinterpret_cast<uint2*>(p_hi + o) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+        *reinterpret_cast<uint2*>(p_mid + o) = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
+        *reinterpret_cast<uint2*>(p_lo + o) = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+    }
+}
+
+// lane l's 16x16x32 operand fragment of rows [16 t, 16 t + 16) of a plane:
+// row l & 15, k = 8 (l >> 4) .. + 7
+__device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ plane, int t, int lane) {
+    return *reinterpret_cast<const bf16x8*>(plane + (16 * t + (lane & 15)) * kGLd + 8 * (lane >> 4));
+}
+
+// B [N, K] fp32 -> three bf16 planes Bs[p][Npad][Kpad] (zero padded), once per GEMM
+__global__ __launch_bounds__(256) void k_split_b(const float* __restrict__ B, int N, int K, int Npad, int Kpad,
+                                                 uint16_t* __restrict__ Bs) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= Npad * Kpad) return;
+    const int n = e / Kpad, k = e % Kpad;
+    const float x = (n < N && k < K) ? B[(size_t)n * K + k] : 0.f;
+    uint32_t h, m, l;
+    split3(x, h, m, l);
+    const size_t plane = (size_t)Npad * Kpad;
+    Bs[e] = (uint16_t)h;
+    Bs[plane + e] = (uint16_t)m;
+    Bs[2 * plane + e] = (uint16_t)l;
+}
+
+template <int NT>
+__global__ __launch_bounds__(kGThreads) void k_gemm_x3(const float* __restrict__ A, const uint16_t* __restrict__ Bs,
+                                                       int Npad, int Kpad, const float* __restrict__ bias,
+                                                       float* __restrict__ C, int M, int N, int K, int relu) {
+    constexpr int BN = 16 * NT;
+    constexpr int AQ = kGBM * (kGBK / 4) / kGThreads;  // float4 of A per thread per k-step (4)
+    __shared__ __attribute__((aligned(16))) uint16_t sA[3][kGBM * kGLd];
+    __shared__ __attribute__((aligned(16))) uint16_t sB[3][BN * kGLd];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int m0 = blockIdx.x * kGBM, n0 = blockIdx.y * BN;
+    const size_t plane = (size_t)Npad * Kpad;
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int c = 0; c < NT; c++) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // A prefetch registers: thread t holds quads e = t + i * 512 (row e / 8, k quad e % 8)
+    float4 pa[AQ];
+    auto load_a = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < AQ; i++) {
+            const int e = threadIdx.x + i * kGThreads;
+            const int gr = m0 + e / (kGBK / 4), gk = k0 + 4 * (e % (kGBK / 4));
+            pa[i] = (gr < M && gk < K) ? *reinterpret_cast<const float4*>(A + (size_t)gr * K + gk)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    load_a(0);
+    for (int k0 = 0; k0 < K; k0 += kGBK) {
+        __syncthreads();  // previous step's fragment reads are done
+        // A: split the prefetched fp32 quads into the three planes
+#pragma unroll
+        for (int i = 0; i < AQ; i++) {
+            const int e = threadIdx.x + i * kGThreads;
+            const int r = e / (kGBK / 4), kq = e % (kGBK / 4);
+            uint32_t h0, m0_, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+            split3(pa[i].x, h0, m0_, l0);
+            split3(pa[i].y, h1, m1, l1);
+            split3(pa[i].z, h2, m2, l2);
+            split3(pa[i].w, h3, m3, l3);
+            const int o = r * kGLd + 4 * kq;
+            *reinterpret_cast<uint2*>(sA[0] + o) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+            *reinterpret_cast<uint2*>(sA[1] + o) = make_uint2(m0_ | (m1 << 16), m2 | (m3 << 16));
+            *reinterpret_cast<uint2*>(sA[2] + o) = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
+        }
+        // B: copy the pre-split planes (16-byte pieces: 4 per 32-k row per plane)
+        for (int e = threadIdx.x; e < 3 * BN * (kGBK / 8); e += kGThreads) {
+            const int p = e / (BN * (kGBK / 8)), rem = e % (BN * (kGBK / 8));
+            const int n = rem / (kGBK / 8), k8 = rem % (kGBK / 8);
+            *reinterpret_cast<uint4*>(sB[p] + n * kGLd + 8 * k8) =
+                *reinterpret_cast<const uint4*>(Bs + p * plane + (size_t)(n0 + n) * Kpad + k0 + 8 * k8);
+        }
+        __syncthreads();
+        if (k0 + kGBK < K) load_a(k0 + kGBK);  // next step's A in flight during the MFMAs
+        bf16x8 a[2][3];
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+#pragma unroll
+            for (int p = 0; p < 3; p++) a[r][p] = frag(sA[p], 2 * wave + r, lane);
+#pragma unroll
+        for (int c = 0; c < NT; c++) {
+            const bf16x8 bh = frag(sB[0], c, lane), bm = frag(sB[1], c, lane), bl = frag(sB[2], c, lane);
+#pragma unroll
+            for (int r = 0; r < 2; r++) {  // small terms first
+                acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][2], bh, acc[r][c], 0, 0, 0);
+                acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], bl, acc[r][c], 0, 0, 0);
+                acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], bm, acc[r][c], 0, 0, 0);
+                acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][1], bh, acc[r][c], 0, 0, 0);
+                acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], bm, acc[r][c], 0, 0, 0);
+                acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[r][0], bh, acc[r][c], 0, 0, 0);
+            }
+        }
+    }
+    // epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + reg
+#pragma unroll
+    for (int c = 0; c < NT; c++) {
+        const int col = n0 + 16 * c + (lane & 15);
+        if (col >= N) continue;
+        const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int row = m0 + 32 * wave + 16 * r + 4 * (lane >> 4) + g;
+                if (row < M) {
+                    float v = acc[r][c][g] + bv;
+                    if (relu) v = v > 0.f ? v : 0.f;
+                    C[(size_t)row * N + col] = v;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace mm
+
+using namespace mm;
+
+static void x3_shape(int N, int K, int* BN, int* Npad, int* Kpad) {
+    *BN = N <= 16 * 17 ? 16 * 17 : 16 * 15;
+    *Npad = (N + *BN - 1) / *BN * *BN;
+    *Kpad = (K + kGBK - 1) / kGBK * kGBK;
+}
+
+extern "C" int mm_gemm_x3_bsplit_len(int N, int K) {
+    int BN, Npad, Kpad;
+    x3_shape(N, K, &BN, &Npad, &Kpad);
+    return 3 * Npad * Kpad;  // uint16 elements
+}
+
+extern "C" int mm_gemm_x3(const float* A, const float* B, const float* bias, float* C, int M, int N, int K, int relu,
+                          uint16_t* bsplit, void* stream) {
+    if (!A || !B || !C || !bsplit || M < 0 || N <= 0 || K <= 0 || (K & 3)) return MM_E_ARG;
+    if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)bsplit) & 15) return MM_E_ARG;
+    if (M == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const int gm = (M + kGBM - 1) / kGBM;
+    int BN, Npad, Kpad;
+    x3_shape(N, K, &BN, &Npad, &Kpad);
+    const bool one = BN == 16 * 17;
+    hipLaunchKernelGGL(k_split_b, dim3((Npad * Kpad + 255) / 256), dim3(256), 0, s, B, N, K, Npad, Kpad, bsplit);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    if (one) {
+        hipLaunchKernelGGL(k_gemm_x3<17>, dim3(gm, 1), dim3(kGThreads), 0, s, A, bsplit, Npad, Kpad, bias, C, M, N, K,
+                           relu);
+    } else {
+        hipLaunchKernelGGL(k_gemm_x3<15>, dim3(gm, Npad / BN), dim3(kGThreads), 0, s, A, bsplit, Npad, Kpad, bias,
+                           C, M, N, K, relu);
+    }
+    return (int)hipGetLastError();
+}

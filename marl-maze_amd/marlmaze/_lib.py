@@ -34,7 +34,8 @@ AF_HAS_MARK = 64
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_gae", "mm_sample", "mm_head_sample",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
-           "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd")
+           "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd",
+           "mm_gemm_x3", "mm_gemm_x3_bsplit_len")
 
 
 class EnvDesc(ctypes.Structure):
@@ -86,6 +87,10 @@ def lib():
         L.mm_sample.restype = i32
         L.mm_head_sample.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P]
         L.mm_head_sample.restype = i32
+        L.mm_gemm_x3.argtypes = [P, P, P, P, i32, i32, i32, i32, P, P]
+        L.mm_gemm_x3_bsplit_len.argtypes = [i32, i32]
+        L.mm_gemm_x3_bsplit_len.restype = i32
+        L.mm_gemm_x3.restype = i32
         L.mm_actor_front_ws_len.restype = i32
         L.mm_actor_front_prep.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), P, P, P, P, P]
         L.mm_actor_front_prep.restype = i32
