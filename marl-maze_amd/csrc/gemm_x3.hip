@@ -12,6 +12,13 @@
 // Six bf16 MFMAs per fp32 product: 2,500 / 6 = 417 TFLOP/s of fp32-accurate
 // peak against 157 for the f32 MFMA.
 //
+// Status: exact to fp32 level (max error vs fp64 2.4-2.8e-7 of sum|ab|, below the
+// fp32 library GEMM's 2.7-3.5e-7), but at 78-85 TFLOP/s effective it does not
+// yet beat the tuned fp32 hipBLASLt kernels (90-110 TFLOP/s) on the MLP
+// shapes: the per-k-step restaging of B (pre-split planes, 1.5x the fp32
+// bytes, re-read by every row block) and LDS bank conflicts dominate
+// (rocprofv3: MFMA busy 22%, waits 62%).  Selected with MARLMAZE_GEMM=x3.
+//
 // Kernel: C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (ReLU), all row-major fp32
 // with K contiguous -- the layout of y = x W^T (nn.Linear forward) and, with
 // B = W^T, of dX = dY W.  Workgroup = 8 waves, tile 256 rows x 16*NT
@@ -28,7 +35,6 @@ namespace mm {
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int kGBM = 256;      // rows per workgroup
 constexpr int kGBK = 32;       // k per step
 constexpr int kGWaves = 8;
 constexpr int kGThreads = kGWaves * 64;
@@ -93,28 +99,37 @@ __global__ __launch_bounds__(256) void k_split_b(const float* __restrict__ B, in
     Bs[2 * plane + e] = (uint16_t)l;
 }
 
+// One workgroup: 4 waves x 32 rows = 128 rows, 16*NT columns.  LDS per
+// workgroup = 3 bf16 planes of A (128 x 80 B) + of B (16 NT x 80 B) <= 80 KB,
+// so two workgroups share a CU: their load/split phases and MFMA phases
+// interleave (one barrier-synchronised workgroup cannot overlap them itself).
+constexpr int kXWaves = 4;
+constexpr int kXThreads = kXWaves * 64;
+constexpr int kXBM = 32 * kXWaves;
+
 template <int NT>
-__global__ __launch_bounds__(kGThreads) void k_gemm_x3(const float* __restrict__ A, const uint16_t* __restrict__ Bs,
-                                                       int Npad, int Kpad, const float* __restrict__ bias,
-                                                       float* __restrict__ C, int M, int N, int K, int relu) {
+__global__ __launch_bounds__(kXThreads, 2) void k_gemm_x3(const float* __restrict__ A,
+                                                          const uint16_t* __restrict__ Bs, int Npad, int Kpad,
+                                                          const float* __restrict__ bias, float* __restrict__ C,
+                                                          int M, int N, int K, int relu) {
     constexpr int BN = 16 * NT;
-    constexpr int AQ = kGBM * (kGBK / 4) / kGThreads;  // float4 of A per thread per k-step (4)
-    __shared__ __attribute__((aligned(16))) uint16_t sA[3][kGBM * kGLd];
+    constexpr int AQ = kXBM * (kGBK / 4) / kXThreads;              // A float4 per thread per k-step (4)
+    constexpr int BPIECES = 3 * BN * (kGBK / 8);                    // 16-byte B pieces per k-step
+    __shared__ __attribute__((aligned(16))) uint16_t sA[3][kXBM * kGLd];
     __shared__ __attribute__((aligned(16))) uint16_t sB[3][BN * kGLd];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int m0 = blockIdx.x * kGBM, n0 = blockIdx.y * BN;
+    const int n0 = blockIdx.x * BN, m0 = blockIdx.y * kXBM;  // column blocks of one row block are adjacent
     const size_t plane = (size_t)Npad * Kpad;
     f32x4 acc[2][NT];
 #pragma unroll
     for (int r = 0; r < 2; r++)
 #pragma unroll
         for (int c = 0; c < NT; c++) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // A prefetch registers: thread t holds quads e = t + i * 512 (row e / 8, k quad e % 8)
-    float4 pa[AQ];
+    float4 pa[AQ];  // next k-step's A (thread t: quads t + 256 i; row e / 8, k quad e % 8)
     auto load_a = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < AQ; i++) {
-            const int e = threadIdx.x + i * kGThreads;
+            const int e = threadIdx.x + i * kXThreads;
             const int gr = m0 + e / (kGBK / 4), gk = k0 + 4 * (e % (kGBK / 4));
             pa[i] = (gr < M && gk < K) ? *reinterpret_cast<const float4*>(A + (size_t)gr * K + gk)
                                        : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -123,10 +138,9 @@ __global__ __launch_bounds__(kGThreads) void k_gemm_x3(const float* __restrict__
     load_a(0);
     for (int k0 = 0; k0 < K; k0 += kGBK) {
         __syncthreads();  // previous step's fragment reads are done
-        // A: split the prefetched fp32 quads into the three planes
 #pragma unroll
-        for (int i = 0; i < AQ; i++) {
-            const int e = threadIdx.x + i * kGThreads;
+        for (int i = 0; i < AQ; i++) {  // A: split into the three planes
+            const int e = threadIdx.x + i * kXThreads;
             const int r = e / (kGBK / 4), kq = e % (kGBK / 4);
             uint32_t h0, m0_, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
             split3(pa[i].x, h0, m0_, l0);
@@ -138,8 +152,7 @@ __global__ __launch_bounds__(kGThreads) void k_gemm_x3(const float* __restrict__
             *reinterpret_cast<uint2*>(sA[1] + o) = make_uint2(m0_ | (m1 << 16), m2 | (m3 << 16));
             *reinterpret_cast<uint2*>(sA[2] + o) = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
         }
-        // B: copy the pre-split planes (16-byte pieces: 4 per 32-k row per plane)
-        for (int e = threadIdx.x; e < 3 * BN * (kGBK / 8); e += kGThreads) {
+        for (int e = threadIdx.x; e < BPIECES; e += kXThreads) {  // B: the pre-split planes (L2-resident)
             const int p = e / (BN * (kGBK / 8)), rem = e % (BN * (kGBK / 8));
             const int n = rem / (kGBK / 8), k8 = rem % (kGBK / 8);
             *reinterpret_cast<uint4*>(sB[p] + n * kGLd + 8 * k8) =
@@ -191,8 +204,9 @@ __global__ __launch_bounds__(kGThreads) void k_gemm_x3(const float* __restrict__
 
 using namespace mm;
 
+// column block width: 144 (N <= 288, e.g. 264 -> 2 blocks) or 160 (460 -> 3 blocks)
 static void x3_shape(int N, int K, int* BN, int* Npad, int* Kpad) {
-    *BN = N <= 16 * 17 ? 16 * 17 : 16 * 15;
+    *BN = N <= 288 ? 16 * 9 : 16 * 10;
     *Npad = (N + *BN - 1) / *BN * *BN;
     *Kpad = (K + kGBK - 1) / kGBK * kGBK;
 }
@@ -209,19 +223,19 @@ extern "C" int mm_gemm_x3(const float* A, const float* B, const float* bias, flo
     if (((uintptr_t)A | (uintptr_t)B | (uintptr_t)bsplit) & 15) return MM_E_ARG;
     if (M == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
-    const int gm = (M + kGBM - 1) / kGBM;
+    const int gm = (M + kXBM - 1) / kXBM;
     int BN, Npad, Kpad;
     x3_shape(N, K, &BN, &Npad, &Kpad);
-    const bool one = BN == 16 * 17;
+    const bool nine = BN == 16 * 9;
     hipLaunchKernelGGL(k_split_b, dim3((Npad * Kpad + 255) / 256), dim3(256), 0, s, B, N, K, Npad, Kpad, bsplit);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    if (one) {
-        hipLaunchKernelGGL(k_gemm_x3<17>, dim3(gm, 1), dim3(kGThreads), 0, s, A, bsplit, Npad, Kpad, bias, C, M, N, K,
-                           relu);
+    if (nine) {
+        hipLaunchKernelGGL(k_gemm_x3<9>, dim3(Npad / BN, gm), dim3(kXThreads), 0, s, A, bsplit, Npad, Kpad, bias, C, M,
+                           N, K, relu);
     } else {
-        hipLaunchKernelGGL(k_gemm_x3<15>, dim3(gm, Npad / BN), dim3(kGThreads), 0, s, A, bsplit, Npad, Kpad, bias,
-                           C, M, N, K, relu);
+        hipLaunchKernelGGL(k_gemm_x3<10>, dim3(Npad / BN, gm), dim3(kXThreads), 0, s, A, bsplit, Npad, Kpad, bias, C,
+                           M, N, K, relu);
     }
     return (int)hipGetLastError();
 }

@@ -14,6 +14,7 @@ so every embedding reads ``x[:, 0:d_i]`` and the actor sees only obs[0:4].
 feature its own slice (what the code evidently intended).
 """
 import ctypes
+import os as _os
 
 import numpy as np
 import torch
@@ -151,8 +152,37 @@ def front_params(projection, attention):
             [attention.querys.weight, attention.keys.weight, attention.values.weight])
 
 
+# MARLMAZE_GEMM=x3 runs the large-M GEMMs of the MLP on the bf16 MFMA with an
+# exact 3-way operand split (csrc/gemm_x3.hip, fp32-class accuracy).  Default:
+# the tuned fp32 library GEMMs, which are still faster on these shapes.
+_X3_MIN_ROWS = 16384
+
+
+def _use_x3(x):
+    return x.is_cuda and x.dim() == 2 and x.shape[0] >= _X3_MIN_ROWS and _os.environ.get("MARLMAZE_GEMM", "lib") == "x3"
+
+
+def gemm_x3(a, b, bias=None, relu=False):
+    """C = a b^T (+ bias) (ReLU): a [M, K], b [N, K] fp32 (mm_gemm_x3)."""
+    from . import _lib
+
+    L = _lib.lib()
+    a = a.contiguous()
+    b = b.contiguous()
+    M, K = a.shape
+    N = b.shape[0]
+    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    ws = torch.empty(L.mm_gemm_x3_bsplit_len(N, K), dtype=torch.int16, device=a.device)
+    bias = bias.contiguous() if bias is not None else None
+    _lib.check(L.mm_gemm_x3(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K, int(relu), _lib.ptr(ws),
+                            _lib.stream_ptr()), "mm_gemm_x3")
+    return c
+
+
 def _linear_fwd(x, w, b, relu):
     """y = x W^T + b (then ReLU), the ReLU in the GEMM epilogue on the GPU."""
+    if _use_x3(x) and w.shape[0] >= 64 and x.shape[1] % 4 == 0:
+        return gemm_x3(x, w, b, relu)
     if relu and x.is_cuda and x.dim() == 2:
         return torch._addmm_activation(b, x, w.t())
     y = F.linear(x, w, b)
@@ -180,7 +210,10 @@ class _SplitKLinear(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         if ctx.relu:
             dy = torch.ops.aten.threshold_backward(dy, y, 0)
-        dx = dy.mm(w)
+        if _use_x3(dy) and w.shape[1] >= 64 and w.shape[0] % 4 == 0:
+            dx = gemm_x3(dy, w.t())  # dX = dY W as a (dY) (W^T)^T
+        else:
+            dx = dy.mm(w)
         M = x.shape[0]
         S = 16 if M >= 16 * 4096 else 1
         if S > 1:
