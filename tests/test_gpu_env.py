@@ -101,13 +101,20 @@ CONFIGS = {
     "main_cfg": dict(default_size=(4, 4), max_timestep=60, rand_sizes=True, rand_range=(12, 13),
                      rand_start=True),
     "d3_rs": dict(default_size=(7, 5), max_timestep=40, rand_start=True, difficulty=3),
+    # edge cases: the largest supported side (41x41 layout), the smallest maze
+    # with an episode end every step (and key/end give-ups), the full size range
+    "21x21_max": dict(default_size=(21, 21), max_timestep=100),
+    "2x2_t1": dict(default_size=(2, 2), max_timestep=1),
+    "rs_2_21": dict(default_size=(5, 5), max_timestep=25, rand_sizes=True, rand_range=(2, 21), rand_start=True,
+                    difficulty=2),
 }
 
 
 @pytest.mark.parametrize("name", list(CONFIGS))
 def test_random_play_matches_oracle(name):
     cfg = CONFIGS[name]
-    n, steps = 2048, 260
+    big = max(cfg["default_size"]) >= 20 or cfg.get("rand_sizes", False)
+    n, steps = (512 if big else 2048), 260  # the C oracle steps large mazes slowly
     seeds = np.arange(n, dtype=np.uint64) * np.uint64(7919) + np.uint64(3)
     env = VecMaze(n, seeds=seeds, **cfg)
     ora = OracleEnv(n, seeds=seeds, **cfg)
@@ -137,6 +144,28 @@ def test_random_play_matches_oracle(name):
         assert np.array_equal(env.agent_state(i), np.stack([ora.agent(i, a) for a in range(2)])), i
         lay = ora.maze(i)["layout"]
         assert np.array_equal(env.layouts()[i], lay), i
+
+
+@pytest.mark.parametrize("n", [1, 33, 100])
+def test_ragged_batch_sizes_match_oracle(n):
+    """Batches that do not fill the 32-maze step tiles (last tile partial)."""
+    cfg = dict(default_size=(10, 10), max_timestep=40)
+    seeds = np.arange(n, dtype=np.uint64) + np.uint64(11)
+    env = VecMaze(n, seeds=seeds, **cfg)
+    ora = OracleEnv(n, seeds=seeds, **cfg)
+    go, gm = env.reset()
+    oo, om = ora.reset_all()
+    assert np.array_equal(go.cpu().numpy(), oo)
+    rng = np.random.default_rng(n)
+    masks = om
+    for s in range(90):
+        act = random_legal(rng, masks)
+        go, gm, gr, gd = env.step(torch.as_tensor(act).cuda(), auto_reset=True)
+        oo, om, orw, od = ora.step_all(act, auto_reset=True)
+        assert np.array_equal(go.cpu().numpy(), oo), s
+        assert np.array_equal(gm.cpu().numpy().astype(bool), om), s
+        assert np.array_equal(gr.cpu().numpy(), orw) and np.array_equal(gd.cpu().numpy().astype(bool), od), s
+        masks = om
 
 
 def test_65536_mazes_10x10_match_oracle():
