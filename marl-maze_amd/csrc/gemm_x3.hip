@@ -36,9 +36,10 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int kGBK = 32;       // k per step
-constexpr int kGWaves = 8;
-constexpr int kGThreads = kGWaves * 64;
-constexpr int kGLd = kGBK + 8;  // bf16 per LDS row (80 B: 16-B reads of a 16-row fragment hit distinct banks)
+constexpr int kGLd = kGBK;  // bf16 per LDS row (64 B), 16-byte chunks XOR-swizzled by (row >> 1) & 3
+// so that fragment reads and both staging writes are bank-conflict free
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * kGLd + 8 * (chunk ^ ((row >> 1) & 3)); }
 
 __device__ __forceinline__ uint32_t bf16_rn(float x) {  // round-to-nearest-even, finite x
     const uint32_t u = __float_as_uint(x);
@@ -54,49 +55,26 @@ __device__ __forceinline__ void split3(float x, uint32_t& hi, uint32_t& mid, uin
     lo = bf16_rn(r2);
 }
 
-// (unused by the pipelined kernel; kept for reference of the plane layout)
-// Stage rows [r0, r0 + rows) x k [k0, k0 + 32) of an fp32 [R, K] matrix into
-// three bf16 planes [rows][kGLd]; out-of-range rows / k are zero.
-__device__ __forceinline__ void stage_split(const float* __restrict__ src, int R, int K, int r0, int k0, int rows,
-                                            uint16_t* __restrict__ p_hi, uint16_t* __restrict__ p_mid,
-                                            uint16_t* __restrict__ p_lo) {
-    const int quads = rows * (kGBK / 4);
-    for (int e = threadIdx.x; e < quads; e += kGThreads) {
-        const int r = e / (kGBK / 4), kq = e % (kGBK / 4);
-        const int gr = r0 + r, gk = k0 + 4 * kq;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gr < R && gk < K) v = *reinterpret_cast<const float4*>(src + (size_t)gr * K + gk);
-        uint32_t h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
-        split3(v.x, h0, m0, l0);
-        split3(v.y, h1, m1, l1);
-        split3(v.z, h2, m2, l2);
-        split3(v.w, h3, m3, l3);
-        const int o = r * kGLd + 4 * kq;
-        *reinterpret_cast<uint2*>(p_hi + o) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
-        *reinterpret_cast<uint2*>(p_mid + o) = make_uint2(m0 | (m1 << 16), m2 | (m3 << 16));
-        *reinterpret_cast<uint2*>(p_lo + o) = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
-    }
-}
-
 // lane l's 16x16x32 operand fragment of rows [16 t, 16 t + 16) of a plane:
 // row l & 15, k = 8 (l >> 4) .. + 7
 __device__ __forceinline__ bf16x8 frag(const uint16_t* __restrict__ plane, int t, int lane) {
-    return *reinterpret_cast<const bf16x8*>(plane + (16 * t + (lane & 15)) * kGLd + 8 * (lane >> 4));
+    return *reinterpret_cast<const bf16x8*>(plane + swz(16 * t + (lane & 15), lane >> 4));
 }
 
-// B [N, K] fp32 -> three bf16 planes Bs[p][Npad][Kpad] (zero padded), once per GEMM
-__global__ __launch_bounds__(256) void k_split_b(const float* __restrict__ B, int N, int K, int Npad, int Kpad,
-                                                 uint16_t* __restrict__ Bs) {
+// B [N, K] fp32 -> pre-split tiles, once per GEMM: for column block cb and
+// k-step ks, one contiguous block Bs[cb][ks][plane][n < BN][32] of bf16 (zero
+// padded), so a workgroup's per-step copy is one linear, coalesced read.
+__global__ __launch_bounds__(256) void k_split_b(const float* __restrict__ B, int N, int K, int BN, int nks,
+                                                 int total, uint16_t* __restrict__ Bs) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= Npad * Kpad) return;
-    const int n = e / Kpad, k = e % Kpad;
-    const float x = (n < N && k < K) ? B[(size_t)n * K + k] : 0.f;
+    if (e >= total) return;
+    const int kk = e % kGBK, n = (e / kGBK) % BN, p = (e / (kGBK * BN)) % 3, ks = (e / (kGBK * BN * 3)) % nks,
+              cb = e / (kGBK * BN * 3 * nks);
+    const int gn = cb * BN + n, gk = ks * kGBK + kk;
+    const float x = (gn < N && gk < K) ? B[(size_t)gn * K + gk] : 0.f;
     uint32_t h, m, l;
     split3(x, h, m, l);
-    const size_t plane = (size_t)Npad * Kpad;
-    Bs[e] = (uint16_t)h;
-    Bs[plane + e] = (uint16_t)m;
-    Bs[2 * plane + e] = (uint16_t)l;
+    Bs[e] = (uint16_t)(p == 0 ? h : (p == 1 ? m : l));
 }
 
 // One workgroup: 4 waves x 32 rows = 128 rows, 16*NT columns.  LDS per
@@ -108,8 +86,8 @@ constexpr int kXThreads = kXWaves * 64;
 constexpr int kXBM = 32 * kXWaves;
 
 template <int NT>
-__global__ __launch_bounds__(kXThreads, 2) void k_gemm_x3(const float* __restrict__ A,
-                                                          const uint16_t* __restrict__ Bs, int Npad, int Kpad,
+__global__ __launch_bounds__(kXThreads, 3) void k_gemm_x3(const float* __restrict__ A,
+                                                          const uint16_t* __restrict__ Bs, int nks,
                                                           const float* __restrict__ bias, float* __restrict__ C,
                                                           int M, int N, int K, int relu) {
     constexpr int BN = 16 * NT;
@@ -119,7 +97,7 @@ __global__ __launch_bounds__(kXThreads, 2) void k_gemm_x3(const float* __restric
     __shared__ __attribute__((aligned(16))) uint16_t sB[3][BN * kGLd];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n0 = blockIdx.x * BN, m0 = blockIdx.y * kXBM;  // column blocks of one row block are adjacent
-    const size_t plane = (size_t)Npad * Kpad;
+    const uint4* btiles = reinterpret_cast<const uint4*>(Bs) + (size_t)blockIdx.x * nks * (BPIECES);
     f32x4 acc[2][NT];
 #pragma unroll
     for (int r = 0; r < 2; r++)
@@ -147,16 +125,17 @@ __global__ __launch_bounds__(kXThreads, 2) void k_gemm_x3(const float* __restric
             split3(pa[i].y, h1, m1, l1);
             split3(pa[i].z, h2, m2, l2);
             split3(pa[i].w, h3, m3, l3);
-            const int o = r * kGLd + 4 * kq;
+            const int o = swz(r, kq >> 1) + 4 * (kq & 1);
             *reinterpret_cast<uint2*>(sA[0] + o) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
             *reinterpret_cast<uint2*>(sA[1] + o) = make_uint2(m0_ | (m1 << 16), m2 | (m3 << 16));
             *reinterpret_cast<uint2*>(sA[2] + o) = make_uint2(l0 | (l1 << 16), l2 | (l3 << 16));
         }
-        for (int e = threadIdx.x; e < BPIECES; e += kXThreads) {  // B: the pre-split planes (L2-resident)
-            const int p = e / (BN * (kGBK / 8)), rem = e % (BN * (kGBK / 8));
-            const int n = rem / (kGBK / 8), k8 = rem % (kGBK / 8);
-            *reinterpret_cast<uint4*>(sB[p] + n * kGLd + 8 * k8) =
-                *reinterpret_cast<const uint4*>(Bs + p * plane + (size_t)(n0 + n) * Kpad + k0 + 8 * k8);
+        {  // B: this k-step's pre-split tile, one contiguous block (coalesced 16-byte pieces)
+            const uint4* bt = btiles + (size_t)(k0 / kGBK) * BPIECES;
+            for (int e = threadIdx.x; e < BPIECES; e += kXThreads) {
+                const int p = e / (BN * (kGBK / 8)), n = (e / (kGBK / 8)) % BN, k8 = e % (kGBK / 8);
+                *reinterpret_cast<uint4*>(sB[p] + swz(n, k8)) = bt[e];
+            }
         }
         __syncthreads();
         if (k0 + kGBK < K) load_a(k0 + kGBK);  // next step's A in flight during the MFMAs
@@ -205,16 +184,16 @@ __global__ __launch_bounds__(kXThreads, 2) void k_gemm_x3(const float* __restric
 using namespace mm;
 
 // column block width: 144 (N <= 288, e.g. 264 -> 2 blocks) or 160 (460 -> 3 blocks)
-static void x3_shape(int N, int K, int* BN, int* Npad, int* Kpad) {
+static void x3_shape(int N, int K, int* BN, int* ncb, int* nks) {
     *BN = N <= 288 ? 16 * 9 : 16 * 10;
-    *Npad = (N + *BN - 1) / *BN * *BN;
-    *Kpad = (K + kGBK - 1) / kGBK * kGBK;
+    *ncb = (N + *BN - 1) / *BN;
+    *nks = (K + kGBK - 1) / kGBK;
 }
 
 extern "C" int mm_gemm_x3_bsplit_len(int N, int K) {
-    int BN, Npad, Kpad;
-    x3_shape(N, K, &BN, &Npad, &Kpad);
-    return 3 * Npad * Kpad;  // uint16 elements
+    int BN, ncb, nks;
+    x3_shape(N, K, &BN, &ncb, &nks);
+    return ncb * nks * 3 * BN * kGBK;  // uint16 elements
 }
 
 extern "C" int mm_gemm_x3(const float* A, const float* B, const float* bias, float* C, int M, int N, int K, int relu,
@@ -224,18 +203,17 @@ extern "C" int mm_gemm_x3(const float* A, const float* B, const float* bias, flo
     if (M == 0) return 0;
     hipStream_t s = (hipStream_t)stream;
     const int gm = (M + kXBM - 1) / kXBM;
-    int BN, Npad, Kpad;
-    x3_shape(N, K, &BN, &Npad, &Kpad);
-    const bool nine = BN == 16 * 9;
-    hipLaunchKernelGGL(k_split_b, dim3((Npad * Kpad + 255) / 256), dim3(256), 0, s, B, N, K, Npad, Kpad, bsplit);
+    int BN, ncb, nks;
+    x3_shape(N, K, &BN, &ncb, &nks);
+    const int total = ncb * nks * 3 * BN * kGBK;
+    hipLaunchKernelGGL(k_split_b, dim3((total + 255) / 256), dim3(256), 0, s, B, N, K, BN, nks, total, bsplit);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    if (nine) {
-        hipLaunchKernelGGL(k_gemm_x3<9>, dim3(Npad / BN, gm), dim3(kXThreads), 0, s, A, bsplit, Npad, Kpad, bias, C, M,
-                           N, K, relu);
+    if (BN == 16 * 9) {
+        hipLaunchKernelGGL(k_gemm_x3<9>, dim3(ncb, gm), dim3(kXThreads), 0, s, A, bsplit, nks, bias, C, M, N, K, relu);
     } else {
-        hipLaunchKernelGGL(k_gemm_x3<10>, dim3(Npad / BN, gm), dim3(kXThreads), 0, s, A, bsplit, Npad, Kpad, bias, C,
-                           M, N, K, relu);
+        hipLaunchKernelGGL(k_gemm_x3<10>, dim3(ncb, gm), dim3(kXThreads), 0, s, A, bsplit, nks, bias, C, M, N, K,
+                           relu);
     }
     return (int)hipGetLastError();
 }
