@@ -152,14 +152,20 @@ def front_params(projection, attention):
             [attention.querys.weight, attention.keys.weight, attention.values.weight])
 
 
-# MARLMAZE_GEMM=x3 runs the large-M GEMMs of the MLP on the bf16 MFMA with an
-# exact 3-way operand split (csrc/gemm_x3.hip, fp32-class accuracy).  Default:
-# the tuned fp32 library GEMMs, which are still faster on these shapes.
+# Large-M GEMMs of the MLP with K, N <= 288 (the 264 x 264 hidden layers, both
+# the forward and the input gradient) run on the bf16 MFMA with an exact 3-way
+# operand split (csrc/gemm_x3.hip, fp32-class accuracy, measured 106 vs 93
+# TFLOP/s for the tuned fp32 library GEMM); the other shapes stay on the
+# library, which is as fast or faster there.  MARLMAZE_GEMM=lib / x3 forces
+# one path for every shape.
 _X3_MIN_ROWS = 16384
 
 
-def _use_x3(x):
-    return x.is_cuda and x.dim() == 2 and x.shape[0] >= _X3_MIN_ROWS and _os.environ.get("MARLMAZE_GEMM", "lib") == "x3"
+def _use_x3(x, n_out, k):
+    mode = _os.environ.get("MARLMAZE_GEMM", "auto")
+    if mode == "lib" or not x.is_cuda or x.dim() != 2 or x.shape[0] < _X3_MIN_ROWS or k % 4 or n_out < 64:
+        return False
+    return mode == "x3" or (n_out <= 288 and k <= 288)
 
 
 def gemm_x3(a, b, bias=None, relu=False):
@@ -181,7 +187,7 @@ def gemm_x3(a, b, bias=None, relu=False):
 
 def _linear_fwd(x, w, b, relu):
     """y = x W^T + b (then ReLU), the ReLU in the GEMM epilogue on the GPU."""
-    if _use_x3(x) and w.shape[0] >= 64 and x.shape[1] % 4 == 0:
+    if _use_x3(x, w.shape[0], x.shape[1]):
         return gemm_x3(x, w, b, relu)
     if relu and x.is_cuda and x.dim() == 2:
         return torch._addmm_activation(b, x, w.t())
@@ -210,7 +216,7 @@ class _SplitKLinear(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         if ctx.relu:
             dy = torch.ops.aten.threshold_backward(dy, y, 0)
-        if _use_x3(dy) and w.shape[1] >= 64 and w.shape[0] % 4 == 0:
+        if _use_x3(dy, w.shape[1], w.shape[0]):
             dx = gemm_x3(dy, w.t())  # dX = dY W as a (dY) (W^T)^T
         else:
             dx = dy.mm(w)
