@@ -115,6 +115,8 @@ def test_random_play_matches_oracle(name):
     cfg = CONFIGS[name]
     big = max(cfg["default_size"]) >= 20 or cfg.get("rand_sizes", False)
     n, steps = (512 if big else 2048), 260  # the C oracle steps large mazes slowly
+    if name == "2x2_t1":  # every step regenerates, and half the 2x2 mazes hit the 65,536-draw give-up
+        n, steps = 256, 24
     seeds = np.arange(n, dtype=np.uint64) * np.uint64(7919) + np.uint64(3)
     env = VecMaze(n, seeds=seeds, **cfg)
     ora = OracleEnv(n, seeds=seeds, **cfg)
