@@ -164,16 +164,37 @@ int mm_gae(const float* reward, const float* value, const uint8_t* done, const f
 int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M, uint64_t seed,
               uint64_t offset, int8_t* actions, float* logp, float* joint_logp, void* stream);
 
-/* C[M, N] = A[M, K] . B[N, K]^T (+ bias[N]) (ReLU if relu != 0), fp32 in and
- * out (row-major, K contiguous, K % 4 == 0, A and B 16-byte aligned), computed
- * on the bf16 MFMA with each operand split exactly into three bf16 parts and
- * the six partial products >= 2^-16 |a b| accumulated in fp32 (csrc/gemm_x3.hip):
- * fp32-class accuracy at 417 TFLOP/s of peak instead of the f32 MFMA's 157.
- * nn.Linear forward: A = x, B = weight.  Input gradient: A = dY, B = weight^T. */
-int mm_gemm_x3(const float* A, const float* B, const float* bias, float* C, int M, int N, int K, int relu,
-               uint16_t* bsplit, void* stream);
-/* uint16 elements of the bsplit scratch mm_gemm_x3 needs for B [N, K]. */
-int mm_gemm_x3_bsplit_len(int N, int K);
+
+/* "TP" operands for the pre-split x3 GEMMs (csrc/x3mlp.hip): a logical [R, C]
+ * fp32 matrix stored as three exact bf16 planes (x = hi + mid + lo) in MFMA
+ * fragment order -- block (rt, ks) of rows 16rt..+15 and columns 32ks..+31 is
+ * 3 x 1 KiB [plane][chunk 4][row 16][8 bf16]; R padded to 256, C to 32, pads
+ * zero.  mm_x3_tp_len: uint16 elements of such a buffer.
+ * mm_x3_tp_pack: fp32 X (row-major with leading dimension ld; trans != 0 reads
+ * element (i, j) at X[j * ld + i]) -> TP.  Replaces nothing in the reference:
+ * the packed form of nn.Linear operands (networks.py:24-36). */
+long mm_x3_tp_len(int R, int C);
+int mm_x3_tp_pack(const float* X, int R, int C, int ld, int trans, uint16_t* tp, void* stream);
+
+/* C = A . B^T (+ bias[N]) (ReLU if relu) (* (mask > 0) if mask), B = TP of
+ * [N, K]: the nn.Linear forward (B = weight) and input gradient (A = dY, B =
+ * TP of weight^T) of networks.py:24-36 / :94-101, with the ReLU-backward of the
+ * layer below fused (mask = that layer's output y [M, ldm]: dX *= (y > 0)).
+ * mm_x3_nt: A = TP of [M, K].  mm_x3_nt_f32a: A fp32 row-major [M, lda]
+ * (K % 4 == 0, lda % 4 == 0, 16-byte aligned), split into bf16 planes inside
+ * the GEMM.  Writes fp32 c [M, ldc] and/or the TP c_tp of [M, N] (N <= 272).
+ * Accuracy: fp32-class (six bf16 MFMA products per fp32 product). */
+int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N, int K, const float* bias, int relu,
+             const float* mask, int ldm, float* c, int ldc, uint16_t* c_tp, void* stream);
+int mm_x3_nt_f32a(const float* a, int lda, const uint16_t* b_tp, int M, int N, int K, const float* bias, int relu,
+                  const float* mask, int ldm, const uint32_t* mbits_in, uint32_t* mbits_out, float* c, int ldc,
+                  uint16_t* c_tp, void* stream);
+/* ReLU masks as bits in the GEMM's accumulator order (N <= 272, fp32 output):
+ * mbits_out (from a forward GEMM with relu) records out > 0; mbits_in (to the
+ * next layer's input-gradient GEMM, same [M, N]) multiplies the output by those
+ * bits -- the ReLU backward (threshold_backward) without re-reading the
+ * activations.  mm_x3_mbits_len: uint32 elements of such a mask for M rows. */
+long mm_x3_mbits_len(int M);
 
 /* The actor's two heads fused with mm_sample: logits =
  * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]

@@ -152,43 +152,85 @@ def front_params(projection, attention):
             [attention.querys.weight, attention.keys.weight, attention.values.weight])
 
 
-# Large-M GEMMs of the MLP with K, N <= 288 (the 264 x 264 hidden layers, both
-# the forward and the input gradient) run on the bf16 MFMA with an exact 3-way
-# operand split (csrc/gemm_x3.hip, fp32-class accuracy, measured 106 vs 93
-# TFLOP/s for the tuned fp32 library GEMM); the other shapes stay on the
-# library, which is as fast or faster there.  MARLMAZE_GEMM=lib / x3 forces
-# one path for every shape.
+# Large-M actor MLP (the 460 -> 264 -> 264 -> 264 ReLU trunk, networks.py:35-36)
+# runs on the x3 GEMMs of csrc/x3mlp.hip: fp32-class accuracy on the bf16 MFMA
+# (each operand split exactly into three bf16 parts, six products kept).  The
+# weights are packed once per call into fragment-order planes (tiny), the
+# activations stay fp32 row-major and are split inside the GEMM.  The forward
+# GEMMs record their ReLU masks as bits; the input-gradient GEMMs of the
+# backward apply them in their epilogue (no threshold_backward pass).  Weight
+# and bias gradients (reductions over all M rows) stay on the library
+# (split-K batched GEMM).  MARLMAZE_GEMM=lib keeps every GEMM on the library.
 _X3_MIN_ROWS = 16384
 
 
-def _use_x3(x, n_out, k):
-    mode = _os.environ.get("MARLMAZE_GEMM", "auto")
-    if mode == "lib" or not x.is_cuda or x.dim() != 2 or x.shape[0] < _X3_MIN_ROWS or k % 4 or n_out < 64:
+def _x3_ok(x, layers):
+    if _os.environ.get("MARLMAZE_GEMM", "auto") == "lib" or not x.is_cuda or x.dim() != 2:
         return False
-    return mode == "x3" or (n_out <= 288 and k <= 288)
+    if x.shape[0] < _X3_MIN_ROWS or x.shape[1] % 4 or x.stride(1) != 1:
+        return False
+    return all(lin.weight.shape[0] <= 272 and lin.weight.shape[1] % 4 == 0 for lin in layers)
 
 
-def gemm_x3(a, b, bias=None, relu=False):
-    """C = a b^T (+ bias) (ReLU): a [M, K], b [N, K] fp32 (mm_gemm_x3)."""
-    from . import _lib
+def _split_k_wgrad(dy, x):
+    """dW = dY^T X over M >> 10^5 rows as an S-way split-K batched GEMM (as one
+    GEMM the [out, in] result has too few tiles to fill 256 CUs)."""
+    M = x.shape[0]
+    S = 16 if M >= 16 * 4096 else 1
+    if S == 1:
+        return dy.t().mm(x)
+    m = M - M % S
+    dw = torch.bmm(dy[:m].view(S, m // S, -1).transpose(1, 2), x[:m].view(S, m // S, -1)).sum(0)
+    if m < M:
+        dw = dw + dy[m:].t().mm(x[m:])
+    return dw
 
-    L = _lib.lib()
-    a = a.contiguous()
-    b = b.contiguous()
-    M, K = a.shape
-    N = b.shape[0]
-    c = torch.empty((M, N), dtype=torch.float32, device=a.device)
-    ws = torch.empty(L.mm_gemm_x3_bsplit_len(N, K), dtype=torch.int16, device=a.device)
-    bias = bias.contiguous() if bias is not None else None
-    _lib.check(L.mm_gemm_x3(_lib.ptr(a), _lib.ptr(b), _lib.ptr(bias), _lib.ptr(c), M, N, K, int(relu), _lib.ptr(ws),
-                            _lib.stream_ptr()), "mm_gemm_x3")
-    return c
+
+class _X3Trunk(torch.autograd.Function):
+    """h3 = relu(W2 relu(W1 relu(W0 h0 + b0) + b1) + b2) on the x3 GEMMs.
+    apply(h0 [M, K0], W0, b0, W1, b1, ...) -> h_last."""
+
+    @staticmethod
+    def forward(ctx, h0, *params):
+        from . import x3
+
+        ws, bs = params[0::2], params[1::2]
+        M, dev = h0.shape[0], h0.device
+        need_grad = any(ctx.needs_input_grad)
+        hs, bits = [h0], []
+        h = h0
+        for w, b in zip(ws, bs):
+            mb = x3.mbits(M, dev) if need_grad else None
+            h, _ = x3.nt(h, x3.pack(w), bias=b, relu=True, mbits_out=mb)
+            hs.append(h)
+            bits.append(mb)
+        if need_grad:
+            ctx.save_for_backward(*hs, *ws)
+            ctx.bits = bits
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        from . import x3
+
+        L = len(ctx.bits)
+        saved = ctx.saved_tensors
+        hs, ws = saved[:L + 1], saved[L + 1:]
+        grads = [None] * (2 * L)
+        dy = torch.ops.aten.threshold_backward(dh.contiguous(), hs[L], 0)  # through the last ReLU
+        dx = None
+        for l in range(L - 1, -1, -1):
+            grads[2 * l] = _split_k_wgrad(dy, hs[l])
+            grads[2 * l + 1] = dy.sum(0)
+            if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0), the mask from layer l-1's forward bits
+                dy, _ = x3.nt(dy, x3.pack(ws[l], trans=True), mbits_in=ctx.bits[l - 1])
+            elif ctx.needs_input_grad[0]:
+                dx, _ = x3.nt(dy, x3.pack(ws[l], trans=True))
+        return (dx, *grads)
 
 
 def _linear_fwd(x, w, b, relu):
     """y = x W^T + b (then ReLU), the ReLU in the GEMM epilogue on the GPU."""
-    if _use_x3(x, w.shape[0], x.shape[1]):
-        return gemm_x3(x, w, b, relu)
     if relu and x.is_cuda and x.dim() == 2:
         return torch._addmm_activation(b, x, w.t())
     y = F.linear(x, w, b)
@@ -196,13 +238,10 @@ def _linear_fwd(x, w, b, relu):
 
 
 class _SplitKLinear(torch.autograd.Function):
-    """nn.Linear (optionally followed by ReLU) whose weight gradient dW = dY^T X
-    (a reduction over all M >> 10^5 rows into a 264 x 460 tile grid) runs as
-    a split-K batched GEMM: S slices of M/S rows each, then a sum over the S
-    partial [out, in] tiles.  As one GEMM the reduction gets only
-    (out/32)*(in/32) output tiles, far fewer than the 256 CUs; split S ways it
-    fills the chip.  With relu=True the forward GEMM applies bias + ReLU in
-    its epilogue and the backward masks dY by y > 0 (threshold_backward)."""
+    """nn.Linear (optionally followed by ReLU) on the library GEMMs, with the
+    weight gradient dW = dY^T X as a split-K batched GEMM (_split_k_wgrad).  With
+    relu=True the forward applies bias + ReLU in the GEMM epilogue and the
+    backward masks dY by y > 0 (threshold_backward)."""
 
     @staticmethod
     def forward(ctx, x, w, b, relu):
@@ -216,26 +255,17 @@ class _SplitKLinear(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         if ctx.relu:
             dy = torch.ops.aten.threshold_backward(dy, y, 0)
-        if _use_x3(dy, w.shape[1], w.shape[0]):
-            dx = gemm_x3(dy, w.t())  # dX = dY W as a (dY) (W^T)^T
-        else:
-            dx = dy.mm(w)
-        M = x.shape[0]
-        S = 16 if M >= 16 * 4096 else 1
-        if S > 1:
-            m = M - M % S
-            dw = torch.bmm(dy[:m].view(S, m // S, -1).transpose(1, 2), x[:m].view(S, m // S, -1)).sum(0)
-            if m < M:
-                dw = dw + dy[m:].t().mm(x[m:])
-        else:
-            dw = dy.t().mm(x)
-        return dx, dw, dy.sum(0), None
+        return dy.mm(w), _split_k_wgrad(dy, x), dy.sum(0), None
 
 
 def _linear(x, w, b, relu=False):
     if x.is_cuda and torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
         return _SplitKLinear.apply(x, w, b, relu)
     return _linear_fwd(x, w, b, relu)
+
+
+class _NoCtx:  # inference: _X3Trunk.forward without autograd bookkeeping
+    needs_input_grad = (False,)
 
 
 class Actor(nn.Module):
@@ -280,7 +310,14 @@ class Actor(nn.Module):
             h = _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
         else:  # host reference path (CPU tests only)
             h = self.attention(self.projection(x))
-        if self.activation is nn.ReLU:
+        if self.activation is nn.ReLU and _x3_ok(h, self.layers):
+            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            if torch.is_grad_enabled() and (h.requires_grad or any(p.requires_grad for p in params)):
+                h = _X3Trunk.apply(h, *params)
+            else:
+                with torch.no_grad():
+                    h = _X3Trunk.forward(_NoCtx(), h, *params)
+        elif self.activation is nn.ReLU:
             for lin in self.layers:
                 h = _linear(h, lin.weight, lin.bias, relu=True)
         else:

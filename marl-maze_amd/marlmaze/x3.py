@@ -1,0 +1,78 @@
+"""Python side of the pre-split x3 GEMMs (csrc/x3mlp.hip, include/marlmaze.h).
+
+A TP tensor is the int16 buffer holding an fp32 [R, C] matrix as three exact
+bf16 planes in MFMA fragment order (R padded to 256, C to 32).  ``TP`` carries
+its logical shape.
+"""
+import torch
+
+from . import _lib
+
+
+class TP:
+    __slots__ = ("buf", "R", "C")
+
+    def __init__(self, R, C, device, buf=None):
+        self.R, self.C = int(R), int(C)
+        n = _lib.lib().mm_x3_tp_len(self.R, self.C)
+        self.buf = buf if buf is not None else torch.empty(n, dtype=torch.int16, device=device)
+        assert self.buf.numel() >= n
+
+    def ptr(self):
+        return _lib.ptr(self.buf)
+
+
+def pack(x, out=None, trans=False):
+    """fp32 [R, C] (or its transpose when trans=True, reading x as [C, R]) -> TP."""
+    assert x.dtype == torch.float32 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
+    R, C = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
+    out = out if out is not None else TP(R, C, x.device)
+    assert (out.R, out.C) == (R, C)
+    _lib.check(_lib.lib().mm_x3_tp_pack(_lib.ptr(x), R, C, x.stride(0), int(trans), out.ptr(), _lib.stream_ptr()),
+               "mm_x3_tp_pack")
+    return out
+
+
+def mbits(M, device):
+    """Buffer for a ReLU bit mask of an [M, N <= 272] GEMM output (accumulator order)."""
+    return torch.empty(_lib.lib().mm_x3_mbits_len(int(M)), dtype=torch.int32, device=device)
+
+
+def nt(a, b, bias=None, relu=False, mask=None, out=None, out_tp=None, want_f32=True, mbits_in=None,
+       mbits_out=None):
+    """C = A B^T (+bias)(ReLU)(* (mask > 0)) with B = TP [N, K] and A either a TP
+    [M, K] or an fp32 row-major [M, K] tensor (split inside the GEMM).  mask: fp32
+    [M, N] (the ReLU output of the layer below).  Returns (fp32 C or None, TP C or None)."""
+    N, K = b.R, b.C
+    if isinstance(a, TP):
+        assert a.C == K, (a.C, K)
+        M, dev = a.R, a.buf.device
+    else:
+        assert a.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1 and a.shape[1] == K, (a.shape, K)
+        M, dev = a.shape[0], a.device
+    if want_f32 and out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=dev)
+    if mask is not None:
+        assert mask.shape == (M, N) and mask.stride(1) == 1
+    ldc = out.stride(0) if out is not None else 0
+    ldm = mask.stride(0) if mask is not None else 0
+    L = _lib.lib()
+    head = (_lib.ptr(bias), int(relu), _lib.ptr(mask), ldm)
+    tail = (_lib.ptr(out), ldc, out_tp.ptr() if out_tp is not None else None, _lib.stream_ptr())
+    if isinstance(a, TP):
+        assert mbits_in is None and mbits_out is None
+        rc = L.mm_x3_nt(a.ptr(), b.ptr(), M, N, K, *head, *tail)
+    else:
+        rc = L.mm_x3_nt_f32a(_lib.ptr(a), a.stride(0), b.ptr(), M, N, K, *head, _lib.ptr(mbits_in),
+                             _lib.ptr(mbits_out), *tail)
+    _lib.check(rc, "mm_x3_nt")
+    return out, out_tp
+
+
+def unpack(tp):
+    """TP -> fp32 [R, C] (hi + mid + lo), with torch ops: for tests and debugging."""
+    Rp, Cp = (tp.R + 255) // 256 * 256, (tp.C + 31) // 32 * 32
+    b = tp.buf[:Rp * Cp * 3].view(Rp // 16, Cp // 32, 3, 4, 16, 8).to(torch.int32) & 0xFFFF
+    f = (b << 16).view(torch.float32)
+    x = f[:, :, 2] + f[:, :, 1] + f[:, :, 0]  # small terms first: exact for a split of an fp32
+    return x.permute(0, 3, 1, 2, 4).reshape(Rp, Cp)[:tp.R, :tp.C]

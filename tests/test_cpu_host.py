@@ -27,7 +27,7 @@ def _ensure_lib():
 
 def test_library_exports_every_declared_symbol():
     _ensure_lib()
-    decl = set(re.findall(r"^\s*int\s+(mm_\w+)\s*\(", open(HEADER).read(), re.M))
+    decl = set(re.findall(r"^\s*(?:int|long)\s+(mm_\w+)\s*\(", open(HEADER).read(), re.M))
     assert decl == set(_lib.EXPORTS), decl ^ set(_lib.EXPORTS)
     L = _lib.lib()
     for sym in decl:
