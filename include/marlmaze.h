@@ -187,14 +187,21 @@ int mm_x3_tp_pack(const float* X, int R, int C, int ld, int trans, uint16_t* tp,
 int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N, int K, const float* bias, int relu,
              const float* mask, int ldm, float* c, int ldc, uint16_t* c_tp, void* stream);
 int mm_x3_nt_f32a(const float* a, int lda, const uint16_t* b_tp, int M, int N, int K, const float* bias, int relu,
-                  const float* mask, int ldm, const uint32_t* mbits_in, uint32_t* mbits_out, float* c, int ldc,
-                  uint16_t* c_tp, void* stream);
+                  const float* mask, int ldm, const uint32_t* mbits_in, uint32_t* mbits_out, float* colsum, float* c,
+                  int ldc, uint16_t* c_tp, void* stream);
 /* ReLU masks as bits in the GEMM's accumulator order (N <= 272, fp32 output):
  * mbits_out (from a forward GEMM with relu) records out > 0; mbits_in (to the
  * next layer's input-gradient GEMM, same [M, N]) multiplies the output by those
  * bits -- the ReLU backward (threshold_backward) without re-reading the
  * activations.  mm_x3_mbits_len: uint32 elements of such a mask for M rows. */
 long mm_x3_mbits_len(int M);
+/* colsum (with mbits_in): per 16-row tile column sums of the output, [ceil(M / 16), N]
+ * -- the next layer down's bias gradient is their column sum (fixed order).
+ * mm_x3_heads_bwd: the actor heads' backward (networks.py:38-41) through the
+ * last ReLU: dY = (dz [M, J] . W [J, N]) * bits (the last forward GEMM's
+ * mbits_out), J <= 8, N <= 272, plus its colsum. */
+int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N, float* dy,
+                    float* colsum, void* stream);
 
 /* The actor's two heads fused with mm_sample: logits =
  * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]

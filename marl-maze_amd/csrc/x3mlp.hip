@@ -118,6 +118,7 @@ struct Epi {
     uint32_t* mbits_out;       // or null: bit = (out > 0) after bias / ReLU
     float* c;                // fp32 [M, ldc] or null
     uint16_t* ctp;           // TP of the output or null (needs one column block)
+    float* colsum;           // EM_BWD, or null: per row tile column sums of the output [rows / 16][N]
     int ldc, ldm, relu, cnks;  // cnks = TP column blocks of the output (ceil(N / 32))
 };
 
@@ -272,6 +273,17 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
             if (EM == EM_F32 && ep.mask && !(ep.mask[(size_t)row * ep.ldm + col] > 0.f)) x = 0.f;
             ep.c[(size_t)row * ep.ldc + col] = x;
         }
+        if (EM == EM_BWD && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
+            float cs = 0.f;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int row = 16 * rt + rq + g;
+                if (row < M && ((bits[(4 * c + g) >> 5] >> ((4 * c + g) & 31)) & 1u)) cs += acc[c][g];
+            }
+            cs += __shfl_xor(cs, 16);
+            cs += __shfl_xor(cs, 32);
+            if (lane < 16 && col < N && 16 * rt < M) ep.colsum[(size_t)rt * N + col] = cs;
+        }
         __builtin_amdgcn_sched_barrier(0);  // one column at a time: bounded live values
     }
     if (EM == EM_FWD) {
@@ -392,6 +404,59 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
     }
 }
 
+// Backward of the actor heads into the last hidden layer (networks.py:38-41 +
+// the ReLU of :36): dY[m, n] = (sum_j dz[m, j] W[j, n]) * bit(m, n), W [J, N]
+// the concatenated head weights, bits the last forward GEMM's ReLU mask.  Same
+// tile map as the GEMM epilogue (one wave per 16-row tile, lane l: rows
+// 4 (l >> 4) + g, columns 16 c + (l & 15)), so the mask bits line up; also the
+// per-tile column sums (the last layer's bias gradient, before the final sum).
+constexpr int kHeadsMaxJ = 8;
+template <int NT>
+__global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz, int J, const float* __restrict__ W,
+                                                   const uint32_t* __restrict__ bits, int M, int N,
+                                                   float* __restrict__ dy, float* __restrict__ colsum) {
+    __shared__ float sw[kHeadsMaxJ][16 * NT];
+    for (int e = threadIdx.x; e < kHeadsMaxJ * 16 * NT; e += blockDim.x) {
+        const int j = e / (16 * NT), n = e % (16 * NT);
+        sw[j][n] = (j < J && n < N) ? W[(size_t)j * N + n] : 0.f;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int rt = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (16 * rt >= M) return;
+    const int rq = 4 * (lane >> 4);
+    float z[4][kHeadsMaxJ];
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+        const int row = 16 * rt + rq + g;
+#pragma unroll
+        for (int j = 0; j < kHeadsMaxJ; j++) z[g][j] = (row < M && j < J) ? dz[(size_t)row * J + j] : 0.f;
+    }
+    uint32_t b[kMaskWords];
+#pragma unroll
+    for (int w = 0; w < kMaskWords; w++) b[w] = bits[((size_t)rt * 64 + lane) * kMaskWords + w];
+#pragma unroll
+    for (int c = 0; c < NT; c++) {
+        const int col = 16 * c + (lane & 15);
+        float cs = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int row = 16 * rt + rq + g, bit = 4 * c + g;
+            float x = 0.f;
+#pragma unroll
+            for (int j = 0; j < kHeadsMaxJ; j++) x = fmaf(z[g][j], sw[j][col], x);
+            if (!((b[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
+            if (row < M && col < N) {
+                dy[(size_t)row * N + col] = x;
+                cs += x;
+            }
+        }
+        cs += __shfl_xor(cs, 16);
+        cs += __shfl_xor(cs, 32);
+        if (lane < 16 && col < N) colsum[(size_t)rt * N + col] = cs;
+    }
+}
+
 }  // namespace x3
 }  // namespace mm
 
@@ -415,7 +480,7 @@ static int persistent_grid() {  // one 16-wave workgroup per CU
     static int cus = 0;
     if (!cus) {
         int dev = 0;
-        hipGetDevice(&dev);
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
     return cus;
@@ -480,7 +545,7 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
     if (e) return e;
     if (!a_tp || ((uintptr_t)a_tp & 15)) return MM_E_ARG;
     if (M == 0) return 0;
-    Epi ep{bias, mask, nullptr, nullptr, c, c_tp, ldc, ldm, relu, rup(N, 32) / 32};
+    Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32};
     return dispatch_nt<ASrcTP>(a_tp, 0, b_tp, M, N, K, ep, (hipStream_t)stream);
 }
 
@@ -488,13 +553,28 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
 // aligned), split into bf16 planes in registers inside the GEMM.
 extern "C" int mm_x3_nt_f32a(const float* a, int lda, const uint16_t* b_tp, int M, int N, int K, const float* bias,
                              int relu, const float* mask, int ldm, const uint32_t* mbits_in, uint32_t* mbits_out,
-                             float* c, int ldc, uint16_t* c_tp, void* stream) {
+                             float* colsum, float* c, int ldc, uint16_t* c_tp, void* stream) {
     int e = check_common(b_tp, M, N, K, mask, ldm, c, ldc, c_tp);
     if (e) return e;
     if (!a || (K & 3) || (lda & 3) || lda < K || ((uintptr_t)a & 15)) return MM_E_ARG;
     if ((mbits_in || mbits_out) && (N > 16 * 17 || c_tp || mask || (mbits_in && mbits_out))) return MM_E_ARG;
     if (mbits_in && (bias || relu)) return MM_E_ARG;  // the input-gradient form: no bias, no ReLU of its own
+    if (colsum && (!mbits_in || !c)) return MM_E_ARG;
     if (M == 0) return 0;
-    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, ldc, ldm, relu, rup(N, 32) / 32};
+    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32};
     return dispatch_nt<ASrcF32>(a, lda, b_tp, M, N, K, ep, (hipStream_t)stream);
+}
+
+// dY = (dz W) * bits (the heads' backward through the last ReLU, bits from the
+// last forward GEMM's mbits_out, N <= 272, J <= 8), and the per-16-row-tile
+// column sums colsum [ceil(M / 16), N].
+extern "C" int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N, float* dy,
+                               float* colsum, void* stream) {
+    if (!dz || !W || !bits || !dy || !colsum || J <= 0 || J > kHeadsMaxJ || N <= 0 || N > 272 || M < 0)
+        return MM_E_ARG;
+    if (M == 0) return 0;
+    const int nrt = (M + 15) / 16;
+    hipLaunchKernelGGL(k_heads_bwd<17>, dim3((nrt + 3) / 4), dim3(256), 0, (hipStream_t)stream, dz, J, W, bits, M, N,
+                       dy, colsum);
+    return (int)hipGetLastError();
 }

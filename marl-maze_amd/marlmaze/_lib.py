@@ -35,7 +35,8 @@ EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_gae", "mm_sample", "mm_head_sample",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd",
-           "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len")
+           "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
+           "mm_x3_heads_bwd")
 
 
 class EnvDesc(ctypes.Structure):
@@ -93,7 +94,9 @@ def lib():
         L.mm_x3_tp_pack.restype = i32
         L.mm_x3_nt.argtypes = [P, P, i32, i32, i32, P, i32, P, i32, P, i32, P, P]
         L.mm_x3_nt.restype = i32
-        L.mm_x3_nt_f32a.argtypes = [P, i32, P, i32, i32, i32, P, i32, P, i32, P, P, P, i32, P, P]
+        L.mm_x3_nt_f32a.argtypes = [P, i32, P, i32, i32, i32, P, i32, P, i32, P, P, P, P, i32, P, P]
+        L.mm_x3_heads_bwd.argtypes = [P, i32, P, P, i32, i32, P, P, P]
+        L.mm_x3_heads_bwd.restype = i32
         L.mm_x3_mbits_len.argtypes = [i32]
         L.mm_x3_mbits_len.restype = ctypes.c_long
         L.mm_x3_nt_f32a.restype = i32

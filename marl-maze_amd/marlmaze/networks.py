@@ -186,28 +186,32 @@ def _split_k_wgrad(dy, x):
     return dw
 
 
+def _x3_trunk_fwd(h0, ws, bs, need_bits):
+    """The ReLU trunk on the x3 GEMMs; returns the activations [h0, h1, ...] and
+    the forward GEMMs' ReLU bit masks (None without need_bits)."""
+    from . import x3
+
+    M, dev = h0.shape[0], h0.device
+    hs, bits = [h0], []
+    h = h0
+    for w, b in zip(ws, bs):
+        mb = x3.mbits(M, dev) if need_bits else None
+        h, _ = x3.nt(h, x3.pack(w), bias=b, relu=True, mbits_out=mb)
+        hs.append(h)
+        bits.append(mb)
+    return hs, bits
+
+
 class _X3Trunk(torch.autograd.Function):
-    """h3 = relu(W2 relu(W1 relu(W0 h0 + b0) + b1) + b2) on the x3 GEMMs.
-    apply(h0 [M, K0], W0, b0, W1, b1, ...) -> h_last."""
+    """The trunk alone with autograd (Actor.trunk under grad; the update uses
+    _X3Actor).  apply(h0, W0, b0, W1, b1, ...) -> h_last."""
 
     @staticmethod
     def forward(ctx, h0, *params):
-        from . import x3
-
-        ws, bs = params[0::2], params[1::2]
-        M, dev = h0.shape[0], h0.device
-        need_grad = any(ctx.needs_input_grad)
-        hs, bits = [h0], []
-        h = h0
-        for w, b in zip(ws, bs):
-            mb = x3.mbits(M, dev) if need_grad else None
-            h, _ = x3.nt(h, x3.pack(w), bias=b, relu=True, mbits_out=mb)
-            hs.append(h)
-            bits.append(mb)
-        if need_grad:
-            ctx.save_for_backward(*hs, *ws)
-            ctx.bits = bits
-        return h
+        hs, bits = _x3_trunk_fwd(h0, params[0::2], params[1::2], True)
+        ctx.save_for_backward(*hs, *params[0::2])
+        ctx.bits = bits
+        return hs[-1]
 
     @staticmethod
     def backward(ctx, dh):
@@ -218,15 +222,62 @@ class _X3Trunk(torch.autograd.Function):
         hs, ws = saved[:L + 1], saved[L + 1:]
         grads = [None] * (2 * L)
         dy = torch.ops.aten.threshold_backward(dh.contiguous(), hs[L], 0)  # through the last ReLU
+        cs = None
         dx = None
         for l in range(L - 1, -1, -1):
             grads[2 * l] = _split_k_wgrad(dy, hs[l])
-            grads[2 * l + 1] = dy.sum(0)
-            if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0), the mask from layer l-1's forward bits
-                dy, _ = x3.nt(dy, x3.pack(ws[l], trans=True), mbits_in=ctx.bits[l - 1])
+            grads[2 * l + 1] = dy.sum(0) if cs is None else cs.sum(0)
+            wt = x3.pack(ws[l], trans=True)
+            if l > 0:
+                cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
+                dy, _ = x3.nt(dy, wt, mbits_in=ctx.bits[l - 1], colsum=cs)
             elif ctx.needs_input_grad[0]:
-                dx, _ = x3.nt(dy, x3.pack(ws[l], trans=True))
+                dx, _ = x3.nt(dy, wt)
         return (dx, *grads)
+
+
+class _X3Actor(torch.autograd.Function):
+    """The actor MLP on the x3 GEMMs: trunk (networks.py:35-36) + heads (:38-41).
+    apply(h0 [M, K0], Wh [J, K], bh [J], W0, b0, W1, b1, ...) -> logits [M, J].
+
+    Backward: the heads' gradient goes through the last ReLU in one kernel
+    (mm_x3_heads_bwd, using the last forward GEMM's ReLU bits); each
+    input-gradient GEMM applies the ReLU bits of the layer below in its
+    epilogue and emits per-tile column sums (that layer's bias gradient); weight
+    gradients are split-K library GEMMs."""
+
+    @staticmethod
+    def forward(ctx, h0, wh, bh, *params):
+        ws, bs = params[0::2], params[1::2]
+        hs, bits = _x3_trunk_fwd(h0, ws, bs, True)
+        z = torch.addmm(bh, hs[-1], wh.t())
+        ctx.save_for_backward(*hs, wh, *ws)
+        ctx.bits = bits
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        from . import x3
+
+        L = len(ctx.bits)
+        saved = ctx.saved_tensors
+        hs, wh, ws = saved[:L + 1], saved[L + 1], saved[L + 2:]
+        dz = dz.contiguous()
+        dwh = _split_k_wgrad(dz, hs[L])
+        dbh = dz.sum(0)
+        dy, cs = x3.heads_bwd(dz, wh, ctx.bits[L - 1])  # through the last ReLU
+        grads = [None] * (2 * L)
+        dx = None
+        for l in range(L - 1, -1, -1):
+            grads[2 * l] = _split_k_wgrad(dy, hs[l])
+            grads[2 * l + 1] = cs.sum(0)
+            wt = x3.pack(ws[l], trans=True)
+            if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0): the ReLU bits of layer l-1's forward
+                cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
+                dy, _ = x3.nt(dy, wt, mbits_in=ctx.bits[l - 1], colsum=cs)
+            elif ctx.needs_input_grad[0]:
+                dx, _ = x3.nt(dy, wt)
+        return (dx, dwh, dbh, *grads)
 
 
 def _linear_fwd(x, w, b, relu):
@@ -264,10 +315,6 @@ def _linear(x, w, b, relu=False):
     return _linear_fwd(x, w, b, relu)
 
 
-class _NoCtx:  # inference: _X3Trunk.forward without autograd bookkeeping
-    needs_input_grad = (False,)
-
-
 class Actor(nn.Module):
     """networks.py:13-48.  forward(x) -> [move_logits [B,5], mark_logit [B,1]]."""
 
@@ -298,26 +345,37 @@ class Actor(nn.Module):
                 torch.cat([self.move_head.bias, self.mark_head.bias], 0))
 
     def forward(self, x):
-        h = self.trunk(x)
         w, b = self.heads()
-        heads = _linear(h, w, b)
+        h = self._front(x)
+        params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+        if self.activation is nn.ReLU and _x3_ok(h, self.layers) and torch.is_grad_enabled() and (
+                h.requires_grad or any(p.requires_grad for p in params)):
+            heads = _X3Actor.apply(h, w, b, *params)  # trunk + heads, fused backward
+        else:
+            heads = _linear(self._mlp(h), w, b)
         return [heads[:, :5], heads[:, 5:6]]
 
     def trunk(self, x):
         """Everything up to the last hidden layer (networks.py:31-36)."""
+        return self._mlp(self._front(x))
+
+    def _front(self, x):
+        """Projection + attention (networks.py:31-34)."""
         x = torch.as_tensor(x, dtype=torch.float32, device=self.move_head.weight.device).reshape(-1, OBS_SPACE)
         if x.is_cuda:  # product path: fused HIP front-end (no fallback on the GPU)
-            h = _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
-        else:  # host reference path (CPU tests only)
-            h = self.attention(self.projection(x))
+            return _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
+        return self.attention(self.projection(x))  # host reference path (CPU tests only)
+
+    def _mlp(self, h):
+        """The hidden layers (networks.py:35-36)."""
         if self.activation is nn.ReLU and _x3_ok(h, self.layers):
             params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
             if torch.is_grad_enabled() and (h.requires_grad or any(p.requires_grad for p in params)):
-                h = _X3Trunk.apply(h, *params)
-            else:
-                with torch.no_grad():
-                    h = _X3Trunk.forward(_NoCtx(), h, *params)
-        elif self.activation is nn.ReLU:
+                return _X3Trunk.apply(h, *params)
+            with torch.no_grad():
+                hs, _ = _x3_trunk_fwd(h, params[0::2], params[1::2], False)
+            return hs[-1]
+        if self.activation is nn.ReLU:
             for lin in self.layers:
                 h = _linear(h, lin.weight, lin.bias, relu=True)
         else:

@@ -39,7 +39,7 @@ def mbits(M, device):
 
 
 def nt(a, b, bias=None, relu=False, mask=None, out=None, out_tp=None, want_f32=True, mbits_in=None,
-       mbits_out=None):
+       mbits_out=None, colsum=None):
     """C = A B^T (+bias)(ReLU)(* (mask > 0)) with B = TP [N, K] and A either a TP
     [M, K] or an fp32 row-major [M, K] tensor (split inside the GEMM).  mask: fp32
     [M, N] (the ReLU output of the layer below).  Returns (fp32 C or None, TP C or None)."""
@@ -64,9 +64,26 @@ def nt(a, b, bias=None, relu=False, mask=None, out=None, out_tp=None, want_f32=T
         rc = L.mm_x3_nt(a.ptr(), b.ptr(), M, N, K, *head, *tail)
     else:
         rc = L.mm_x3_nt_f32a(_lib.ptr(a), a.stride(0), b.ptr(), M, N, K, *head, _lib.ptr(mbits_in),
-                             _lib.ptr(mbits_out), *tail)
+                             _lib.ptr(mbits_out), _lib.ptr(colsum), *tail)
     _lib.check(rc, "mm_x3_nt")
     return out, out_tp
+
+
+def colsum_buf(M, N, device):
+    """Per-16-row-tile column sums [ceil(M / 16), N] (bias-gradient partials)."""
+    return torch.empty(((int(M) + 15) // 16, int(N)), dtype=torch.float32, device=device)
+
+
+def heads_bwd(dz, w, bits):
+    """dY = (dz [M, J] @ w [J, N]) * bits, and its per-tile column sums."""
+    M, J = dz.shape
+    N = w.shape[1]
+    dz, w = dz.contiguous(), w.contiguous()
+    dy = torch.empty((M, N), dtype=torch.float32, device=dz.device)
+    cs = colsum_buf(M, N, dz.device)
+    _lib.check(_lib.lib().mm_x3_heads_bwd(_lib.ptr(dz), J, _lib.ptr(w), _lib.ptr(bits), M, N, _lib.ptr(dy),
+                                          _lib.ptr(cs), _lib.stream_ptr()), "mm_x3_heads_bwd")
+    return dy, cs
 
 
 def unpack(tp):

@@ -281,40 +281,52 @@ def test_x3_relu_bits(M):
     assert torch.equal(dx == 0, (y <= 0) | (ref == 0))
 
 
-def test_x3_trunk_gradients_vs_fp64():
-    """The actor trunk on the x3 GEMMs (forward, ReLU bits, input and weight
-    gradients through _X3Trunk) against an fp64 evaluation of the same trunk
-    linearised at the same ReLU pattern (a ReLU whose input is within fp32
-    rounding of 0 may flip under any change of summation order, for the fp32
-    library GEMMs just as here, so the pattern is taken from the forward under
-    test).  Tolerance: 1e-6 of max|ref| for h, 2e-5 for the gradients (sums
-    over 40,000 rows)."""
+@pytest.mark.parametrize("heads", [False, True])
+def test_x3_trunk_gradients_vs_fp64(heads):
+    """The actor MLP on the x3 GEMMs -- _X3Trunk (trunk) and _X3Actor (trunk +
+    heads: forward, ReLU bits, the fused heads backward, input / weight / bias
+    gradients with the bias sums from the GEMM epilogues) -- against an fp64
+    evaluation linearised at the same ReLU pattern (a ReLU whose input is within
+    fp32 rounding of 0 may flip under any change of summation order, for the
+    fp32 library GEMMs just as here, so the pattern is taken from the forward
+    under test).  Tolerance: 1e-6 of max|ref| for outputs, 2e-5 for gradients
+    (sums over 40,000 rows)."""
     from marlmaze import x3
-    from marlmaze.networks import Actor, _X3Trunk
+    from marlmaze.networks import Actor, _X3Actor, _X3Trunk
 
     torch.manual_seed(1)
     actor = Actor([264, 264, 264]).cuda()
     M = 40000
     h0 = torch.randn(M, 460, device="cuda").requires_grad_(True)
-    dh = torch.randn(M, 264, device="cuda")
     params = [t for lin in actor.layers for t in (lin.weight, lin.bias)]
-    h3 = _X3Trunk.apply(h0, *params)
-    got = [h3.detach()] + list(torch.autograd.grad(h3, [h0] + params, dh))
-    # the x3 forward's activations give the ReLU pattern (the same GEMMs _X3Trunk runs)
-    pattern = []
+    wh, bh = (t.detach().clone().requires_grad_(True) for t in actor.heads())
+    with torch.no_grad():
+        wh.mul_(100.0)  # heads at the scale of the hidden layers (init is x0.01)
+    if heads:
+        dout = torch.randn(M, 6, device="cuda")
+        out = _X3Actor.apply(h0, wh, bh, *params)
+        inputs = [h0, wh, bh] + params
+    else:
+        dout = torch.randn(M, 264, device="cuda")
+        out = _X3Trunk.apply(h0, *params)
+        inputs = [h0] + params
+    got = [out.detach()] + list(torch.autograd.grad(out, inputs, dout))
+    pattern = []  # the x3 forward's ReLU pattern (the same GEMMs the functions run)
     with torch.no_grad():
         h = h0.detach()
         for i in range(3):
             h, _ = x3.nt(h, x3.pack(params[2 * i]), bias=params[2 * i + 1], relu=True)
             pattern.append(h > 0)
-    x64 = h0.detach().double().cpu().requires_grad_(True)
-    p64 = [p.detach().double().cpu().requires_grad_(True) for p in params]
+    in64 = [t.detach().double().cpu().requires_grad_(True) for t in inputs]
+    x64 = in64[0]
+    p64 = in64[3:] if heads else in64[1:]
     h = x64
     for i in range(3):
         h = (h @ p64[2 * i].t() + p64[2 * i + 1]) * pattern[i].cpu()
-    ref = [h.detach()] + list(torch.autograd.grad(h, [x64] + p64, dh.double().cpu()))
-    names = ["h3", "dh0", "dW0", "db0", "dW1", "db1", "dW2", "db2"]
-    for n, a, r in zip(names, got, ref):
-        tol = 1e-6 if n == "h3" else 2e-5
+    if heads:
+        h = h @ in64[1].t() + in64[2]
+    ref = [h.detach()] + list(torch.autograd.grad(h, in64, dout.double().cpu()))
+    for n, (a, r) in enumerate(zip(got, ref)):
+        tol = 1e-6 if n == 0 else 2e-5
         err = (a.double().cpu() - r).abs().max().item() / r.abs().max().item()
         assert err < tol, (n, err)
