@@ -17,7 +17,11 @@
 //
 // TP layout of a logical [R, C] fp32 matrix (R padded to 256, C to 32):
 //   block (rt, ks) = rows 16 rt .. +15, cols 32 ks .. +31, 3 KiB contiguous:
-//   [plane 3][chunk c 4][row r 16][8 bf16]  (element (16rt + r, 32ks + 8c + j))
+//   [plane 3][chunk c 4][row r 16][8 bf16], element j of chunk c = column
+//   32 ks + kcol(c, j), kcol(c, j) = 4 c + j (j < 4) or 16 + 4 c + (j - 4):
+//   the MFMA takes any order of k inside a step as long as both operands use
+//   it, and this one lets a 16-lane group read a row's 64 contiguous bytes
+//   (the fp32 A source below) instead of 16-byte pieces 32 bytes apart.
 // so lane l of a 16x16x32 MFMA operand fragment (row l & 15, k 8 (l >> 4) ..
 // +7) reads the 16 bytes at l * 16 of a plane block: lane-linear, conflict
 // free, and exactly the image one global_load_lds_dwordx4 writes.
@@ -39,6 +43,9 @@ constexpr int kBlk = 1536;  // uint16 per (rt, ks) block: 3 planes x 512
 constexpr int kRowPad = 256;
 
 __host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
+
+// column (inside a 32-wide k-step) of element j of fragment chunk c
+__host__ __device__ inline int kcol(int c, int j) { return j < 4 ? 4 * c + j : 12 + 4 * c + j; }
 
 __device__ __forceinline__ uint32_t bf16_rn(float x) {  // round-to-nearest-even (finite x)
     const uint32_t u = __float_as_uint(x);
@@ -73,11 +80,11 @@ __global__ __launch_bounds__(256) void k_tp_pack(const float* __restrict__ X, in
         const long blk = e >> 6;      // (rt, ks)
         const int ks = (int)(blk % nks);
         const int rt = (int)(blk / nks);
-        const int row = 16 * rt + (l & 15), col0 = 32 * ks + 8 * (l >> 4);
+        const int row = 16 * rt + (l & 15), c = l >> 4;
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            const int col = col0 + j;
+            const int col = 32 * ks + kcol(c, j);
             v[j] = (row < R && col < C) ? (trans ? X[(size_t)col * ld + row] : X[(size_t)row * ld + col]) : 0.f;
         }
         uint4 h, m, lo;
@@ -173,13 +180,13 @@ struct ASrcF32 {  // fp32 row-major [M, lda]: two 16-byte loads per lane, split 
         const int r = 16 * rt + (lane & 15);
         ok = r < M;
         K = K_;
-        row = base + (size_t)(ok ? r : 0) * lda + 8 * (lane >> 4);
+        row = base + (size_t)(ok ? r : 0) * lda + 4 * (lane >> 4);
     }
     __device__ __forceinline__ void load(int ks, Raw& r, int lane) const {
-        const int k = 32 * ks + 8 * (lane >> 4);
+        const int k = 32 * ks + 4 * (lane >> 4);  // kcol(c, 0..3) = 4c.., kcol(c, 4..7) = 16 + 4c..
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         r[0] = (ok && k < K) ? *reinterpret_cast<const float4*>(row + 32 * ks) : z;
-        r[1] = (ok && k + 4 < K) ? *reinterpret_cast<const float4*>(row + 32 * ks + 4) : z;
+        r[1] = (ok && k + 16 < K) ? *reinterpret_cast<const float4*>(row + 32 * ks + 16) : z;
     }
     __device__ __forceinline__ void frag(const Raw& r, bf16x8 (&a)[3]) const {
         uint32_t h[4], m[4], l[4];
@@ -314,13 +321,12 @@ __device__ __forceinline__ void epilogue_tp(const f32x4 (&acc)[NT], float* slice
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const float4 v0 = *reinterpret_cast<const float4*>(slice + rr * 36 + 8 * ch);
-        const float4 v1 = *reinterpret_cast<const float4*>(slice + rr * 36 + 8 * ch + 4);
+        const float4 v0 = *reinterpret_cast<const float4*>(slice + rr * 36 + kcol(ch, 0));
+        const float4 v1 = *reinterpret_cast<const float4*>(slice + rr * 36 + kcol(ch, 4));
         float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        const int colb = 32 * ks + 8 * ch;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            const int col = colb + j;
+            const int col = 32 * ks + kcol(ch, j);
             float x = 0.f;
             if (col < N && row < M) {
                 x = v[j] + (ep.bias ? ep.bias[col] : 0.f);

@@ -92,4 +92,6 @@ def unpack(tp):
     b = tp.buf[:Rp * Cp * 3].view(Rp // 16, Cp // 32, 3, 4, 16, 8).to(torch.int32) & 0xFFFF
     f = (b << 16).view(torch.float32)
     x = f[:, :, 2] + f[:, :, 1] + f[:, :, 0]  # small terms first: exact for a split of an fp32
-    return x.permute(0, 3, 1, 2, 4).reshape(Rp, Cp)[:tp.R, :tp.C]
+    # [rt, ks, chunk c, row, j] -> column 32 ks + kcol(c, j), kcol = 4c + j (j < 4) or 16 + 4c + (j - 4)
+    x = x.view(Rp // 16, Cp // 32, 4, 16, 2, 4).permute(0, 3, 1, 4, 2, 5)  # [rt, row, ks, half, c, q]
+    return x.reshape(Rp, Cp)[:tp.R, :tp.C]
