@@ -203,6 +203,21 @@ long mm_x3_mbits_len(int M);
 int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N, float* dy,
                     float* colsum, void* stream);
 
+/* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
+ * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),
+ * masks [2M, 6] u8, actions [2M, 2] i8 (move, mark); per sample the joint
+ * log-prob (sum over the two agents of the masked log-softmax of the move and
+ * the masked Bernoulli log-prob of the mark), ratio = exp(logp - old_logp),
+ * term = min(ratio A, clamp(ratio, 1 - clip, 1 + clip) A).
+ * mm_ppo_loss: partial [mm_ppo_loss_partials(M)] per-workgroup sums of term
+ * (the loss is -sum(partial) / M) and coef [M] = d loss / d logp.
+ * mm_ppo_loss_bwd: dheads [2M, 6] = dloss[0] * coef * d logp / d heads. */
+int mm_ppo_loss_partials(int M);
+int mm_ppo_loss(const float* heads, const uint8_t* masks, const int8_t* actions, const float* old_logp,
+                const float* adv, int M, float clip, float* coef, float* partial, void* stream);
+int mm_ppo_loss_bwd(const float* heads, const uint8_t* masks, const int8_t* actions, const float* coef,
+                    const float* dloss, int M, float* dheads, void* stream);
+
 /* The actor's two heads fused with mm_sample: logits =
  * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]
  * [6, K] and b [6] (networks.py:38-41), then the draw of mm_sample with the

@@ -13,6 +13,13 @@
 //             counter-based Philox4x32-10 draws.
 //   k_head_sample  the actor's two heads (networks.py:38-41) fused with
 //             k_sample's draw: last hidden layer -> actions, log-probs.
+//   k_ppo_loss / k_ppo_loss_bwd  the update's policy side (PPO.py:62-72 with
+//             get_log_probs PPO.py:154-168): per-agent masked log-softmax of
+//             the move logits + masked Bernoulli mark log-prob, joint log-prob,
+//             ratio, clipped surrogate and its mean; the backward writes the
+//             gradient of the loss w.r.t. the six head logits of each agent
+//             row directly (torch's min() splits a tie's gradient in half, as
+//             here).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -220,6 +227,92 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* 
     if (joint && valid && j == 0 && (row & 1) == 0) joint[row >> 1] = lp + (row + 1 < M ? other : 0.f);
 }
 
+// per agent row: log pi(a | z) for the masked move logits z[0:5] and the
+// masked mark logit z[5] (PPO.py:154-168, torch's op order in fp32); also the
+// gradient d log pi / d z when grad != null
+__device__ __forceinline__ float row_logp(const float* z, const uint8_t* mk, int move, int mark, float* grad) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 5; j++)
+        if (mk[j]) mx = fmaxf(mx, z[j]);
+    float se = 0.f;
+    float e[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        e[j] = mk[j] ? expf(z[j] - mx) : 0.f;
+        se += e[j];
+    }
+    const float lse = logf(se);
+    const float lpm = mk[move] ? (z[move] - mx) - lse : -INFINITY;  // log_softmax(masked)[move]
+    // mark: p = sigmoid(masked logit); log(p) or log(1 - p)
+    const float k = mk[5] ? z[5] : -INFINITY;
+    const float p = 1.f / (1.f + expf(-k));
+    const float pm = mark ? p : 1.f - p;
+    if (grad) {
+        const float inv = 1.f / se;
+#pragma unroll
+        for (int j = 0; j < 5; j++) grad[j] = mk[j] ? ((j == move ? 1.f : 0.f) - e[j] * inv) : 0.f;
+        grad[5] = mk[5] ? (mark ? 1.f - p : -p) : 0.f;
+    }
+    return lpm + logf(pm);
+}
+
+constexpr int kLossThreads = 256;
+
+// one thread per sample (two agent rows); per-workgroup partial sums of the
+// clipped surrogate (fixed order: deterministic), coef[i] = d(-mean term)/d logp_i
+__global__ __launch_bounds__(kLossThreads) void k_ppo_loss(const float* __restrict__ z, const uint8_t* __restrict__ mk,
+                                                           const int8_t* __restrict__ act,
+                                                           const float* __restrict__ old_lp,
+                                                           const float* __restrict__ adv, int M, float clip,
+                                                           float* __restrict__ coef, float* __restrict__ partial) {
+    __shared__ float red[kLossThreads];
+    const int i = blockIdx.x * kLossThreads + threadIdx.x;
+    float term = 0.f;
+    if (i < M) {
+        float lp = 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; a++) {
+            const int r = 2 * i + a;
+            lp += row_logp(z + (size_t)r * 6, mk + (size_t)r * 6, act[2 * r], act[2 * r + 1], nullptr);
+        }
+        const float ratio = expf(lp - old_lp[i]);
+        const float A = adv[i];
+        const float s1 = ratio * A;
+        const float rc = fminf(fmaxf(ratio, 1.f - clip), 1.f + clip);
+        const float s2 = rc * A;
+        term = fminf(s1, s2);
+        // torch.min backward: the smaller input gets the gradient, a tie splits it;
+        // clamp passes it only inside [1 - clip, 1 + clip]
+        const bool inside = ratio >= 1.f - clip && ratio <= 1.f + clip;
+        float dd;
+        if (s1 < s2) dd = A;
+        else if (s1 > s2) dd = inside ? A : 0.f;
+        else dd = 0.5f * A + (inside ? 0.5f * A : 0.f);
+        coef[i] = -dd * ratio / (float)M;
+    }
+    red[threadIdx.x] = term;
+    __syncthreads();
+    for (int w = kLossThreads / 2; w > 0; w >>= 1) {
+        if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void k_ppo_loss_bwd(const float* __restrict__ z, const uint8_t* __restrict__ mk,
+                                                      const int8_t* __restrict__ act, const float* __restrict__ coef,
+                                                      const float* __restrict__ dloss, int M,
+                                                      float* __restrict__ dz) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;  // agent row
+    if (r >= 2 * M) return;
+    float g[6];
+    row_logp(z + (size_t)r * 6, mk + (size_t)r * 6, act[2 * r], act[2 * r + 1], g);
+    const float c = coef[r >> 1] * dloss[0];
+#pragma unroll
+    for (int j = 0; j < 6; j++) dz[(size_t)r * 6 + j] = c * g[j];
+}
+
 }  // namespace mm
 
 using namespace mm;
@@ -254,5 +347,23 @@ extern "C" int mm_head_sample(const float* h, int ldh, int K, const float* w, co
     hipLaunchKernelGGL(k_head_sample, dim3((M + kHsRows - 1) / kHsRows), dim3(kHsLanes * kHsRows), 0,
                        (hipStream_t)stream, h, ldh, K, w, b, masks, M, seed, offset, actions, logp, joint_logp,
                        logits);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_ppo_loss_partials(int M) { return (M + kLossThreads - 1) / kLossThreads; }
+
+extern "C" int mm_ppo_loss(const float* heads, const uint8_t* masks, const int8_t* actions, const float* old_logp,
+                           const float* adv, int M, float clip, float* coef, float* partial, void* stream) {
+    if (!heads || !masks || !actions || !old_logp || !adv || !coef || !partial || M <= 0) return MM_E_ARG;
+    hipLaunchKernelGGL(k_ppo_loss, dim3(mm_ppo_loss_partials(M)), dim3(kLossThreads), 0, (hipStream_t)stream, heads,
+                       masks, actions, old_logp, adv, M, clip, coef, partial);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_ppo_loss_bwd(const float* heads, const uint8_t* masks, const int8_t* actions, const float* coef,
+                               const float* dloss, int M, float* dheads, void* stream) {
+    if (!heads || !masks || !actions || !coef || !dloss || !dheads || M <= 0) return MM_E_ARG;
+    hipLaunchKernelGGL(k_ppo_loss_bwd, dim3((2 * M + 255) / 256), dim3(256), 0, (hipStream_t)stream, heads, masks,
+                       actions, coef, dloss, M, dheads);
     return (int)hipGetLastError();
 }

@@ -41,6 +41,41 @@ from .vecmaze import VecMaze
 MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
 
 
+class _PolicyLoss(torch.autograd.Function):
+    """-mean(min(r A, clamp(r, 1-clip, 1+clip) A)), r = exp(logp - old_logp),
+    logp = sum over the two agents of get_log_probs (PPO.py:62-72, 154-168),
+    straight from the [2M, 6] head logits (mm_ppo_loss, mm_ppo_loss_bwd)."""
+
+    @staticmethod
+    def forward(ctx, heads, masks, act, old_logp, adv, clip):
+        from . import _lib
+
+        L = _lib.lib()
+        M = old_logp.shape[0]
+        heads = heads.contiguous()
+        mk = masks.contiguous().view(torch.uint8) if masks.dtype == torch.bool else masks.to(torch.uint8).contiguous()
+        a8 = act.to(torch.int8).contiguous()
+        coef = torch.empty(M, dtype=torch.float32, device=heads.device)
+        part = torch.empty(L.mm_ppo_loss_partials(M), dtype=torch.float32, device=heads.device)
+        _lib.check(L.mm_ppo_loss(_lib.ptr(heads), _lib.ptr(mk), _lib.ptr(a8), _lib.ptr(old_logp.contiguous()),
+                                 _lib.ptr(adv.contiguous()), M, float(clip), _lib.ptr(coef), _lib.ptr(part),
+                                 _lib.stream_ptr()), "mm_ppo_loss")
+        ctx.save_for_backward(heads, mk, a8, coef)
+        return -part.sum() / M
+
+    @staticmethod
+    def backward(ctx, dloss):
+        from . import _lib
+
+        heads, mk, a8, coef = ctx.saved_tensors
+        dz = torch.empty_like(heads)
+        dl = dloss.reshape(1).to(torch.float32).contiguous()
+        _lib.check(_lib.lib().mm_ppo_loss_bwd(_lib.ptr(heads), _lib.ptr(mk), _lib.ptr(a8), _lib.ptr(coef),
+                                              _lib.ptr(dl), coef.shape[0], _lib.ptr(dz), _lib.stream_ptr()),
+                   "mm_ppo_loss_bwd")
+        return dz, None, None, None, None, None
+
+
 class PPO:
     def __init__(self, agent_amount, epochs=500, batch_size=15000, lr=0.0002, discount_rate=0.99, lam=0.95,
                  updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
@@ -206,11 +241,17 @@ class PPO:
 
     def minibatch_step(self, obs, act, old_logp, adv, rtg, masks):
         V = self.critic(obs).view(-1)
-        cur = self.policy_logp(obs, act, masks)
-        ratio = torch.exp(cur - old_logp)
-        s1 = ratio * adv
-        s2 = torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv
-        actor_loss = -torch.mean(torch.min(s1, s2))
+        M = obs.shape[0]
+        if obs.is_cuda:  # PPO.py:62-72 as two kernels (mm_ppo_loss / _bwd) on the [2M, 6] head logits
+            heads = self.actor.logits(obs.reshape(2 * M, 65))
+            actor_loss = _PolicyLoss.apply(heads, masks.reshape(2 * M, 6), act.reshape(2 * M, 2), old_logp, adv,
+                                           self.clip)
+        else:
+            cur = self.policy_logp(obs, act, masks)
+            ratio = torch.exp(cur - old_logp)
+            s1 = ratio * adv
+            s2 = torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv
+            actor_loss = -torch.mean(torch.min(s1, s2))
         critic_loss = torch.nn.functional.mse_loss(V, rtg)
         self.actor_optim.zero_grad(set_to_none=True)  # backward assigns fresh gradients: no fill + add launches
         self.critic_optim.zero_grad(set_to_none=True)
@@ -241,6 +282,9 @@ class PPO:
         order = index_list[:used]
         p_obs, p_act, p_logp, p_advs, p_rtgs, p_masks = (t[order] for t in (b_obs, b_act, b_logp, b_advs, b_rtgs,
                                                                           b_masks))
+        if p_obs.is_cuda:  # the fused policy-loss kernels take int8 actions and u8 masks: convert once
+            p_act = p_act.to(torch.int8)
+            p_masks = p_masks.view(torch.uint8) if p_masks.dtype == torch.bool else p_masks.to(torch.uint8)
         hist = []
         for _ in range(self.updates_per_batch):
             self.decay_lr()

@@ -345,15 +345,18 @@ class Actor(nn.Module):
                 torch.cat([self.move_head.bias, self.mark_head.bias], 0))
 
     def forward(self, x):
+        heads = self.logits(x)
+        return [heads[:, :5], heads[:, 5:6]]
+
+    def logits(self, x):
+        """[B, 6] = [5 move logits | mark logit] (both heads of networks.py:38-41)."""
         w, b = self.heads()
         h = self._front(x)
         params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
         if self.activation is nn.ReLU and _x3_ok(h, self.layers) and torch.is_grad_enabled() and (
                 h.requires_grad or any(p.requires_grad for p in params)):
-            heads = _X3Actor.apply(h, w, b, *params)  # trunk + heads, fused backward
-        else:
-            heads = _linear(self._mlp(h), w, b)
-        return [heads[:, :5], heads[:, 5:6]]
+            return _X3Actor.apply(h, w, b, *params)  # trunk + heads, fused backward
+        return _linear(self._mlp(h), w, b)
 
     def trunk(self, x):
         """Everything up to the last hidden layer (networks.py:31-36)."""

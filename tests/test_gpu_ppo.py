@@ -330,3 +330,42 @@ def test_x3_trunk_gradients_vs_fp64(heads):
         tol = 1e-6 if n == 0 else 2e-5
         err = (a.double().cpu() - r).abs().max().item() / r.abs().max().item()
         assert err < tol, (n, err)
+
+
+@pytest.mark.parametrize("M", [1, 300, 20000])
+def test_fused_policy_loss_matches_torch(M):
+    """mm_ppo_loss / mm_ppo_loss_bwd (PPO.py:62-72 with get_log_probs
+    PPO.py:154-168) == the torch formula on the same head logits: loss at 1e-6
+    relative, d loss / d heads at 1e-6 of its max.  Ratios are spread around the
+    clip range so that both sides of min() and the clamp's edges are exercised."""
+    from marlmaze.PPO import _PolicyLoss
+
+    g = torch.Generator(device="cuda").manual_seed(M)
+    heads = torch.randn(2 * M, 6, device="cuda", generator=g) * 2
+    masks = torch.rand(2 * M, 6, device="cuda", generator=g) < 0.7
+    masks[:, 4] = True  # stay is always legal (maze_agent.py:136)
+    mv = torch.where(masks[:, :5], torch.rand(2 * M, 5, device="cuda", generator=g), torch.zeros(())).argmax(1)
+    mark = (torch.rand(2 * M, device="cuda", generator=g) < 0.5) & masks[:, 5]
+    act = torch.stack([mv, mark.long()], 1)
+    adv = torch.randn(M, device="cuda", generator=g)
+
+    def logp_torch(z):
+        ml = z[:, :5].masked_fill(~masks[:, :5], float("-inf"))
+        lp = torch.log_softmax(ml, -1).gather(1, act[:, 0:1]).squeeze(1)
+        kl = z[:, 5].masked_fill(~masks[:, 5], float("-inf"))
+        p = torch.sigmoid(kl)
+        p = torch.where(act[:, 1] != 0, p, 1 - p)
+        return (lp + torch.log(p)).view(M, 2).sum(1)
+
+    with torch.no_grad():
+        old = logp_torch(heads) + torch.randn(M, device="cuda", generator=g) * 0.3  # ratios around 1
+    z1 = heads.clone().requires_grad_(True)
+    cur = logp_torch(z1)
+    r = torch.exp(cur - old)
+    ref = -torch.mean(torch.min(r * adv, torch.clamp(r, 0.8, 1.2) * adv))
+    gref, = torch.autograd.grad(ref, z1)
+    z2 = heads.clone().requires_grad_(True)
+    loss = _PolicyLoss.apply(z2, masks, act.to(torch.int8), old, adv, 0.2)
+    got, = torch.autograd.grad(loss, z2)
+    assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item()) + 1e-7, (loss.item(), ref.item())
+    assert (got - gref).abs().max().item() <= 1e-6 * gref.abs().max().item() + 1e-9
