@@ -15,7 +15,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "tools", "_build", "libmarlmaze_stamps.so")
+OUT = os.path.join(ROOT, "tools", "_var", "libmarlmaze_stamps.so")  # git-ignored; travels to the GPU box
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--build", action="store_true")
