@@ -313,12 +313,12 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
 // ---------------------------------------------------------------------------
 // LDS per sample (floats): attention phase {K 23x10 | Q 23x10 | V 23x20 |
 // P 23x23 | dS 23x23}; after a barrier the same words hold the reduction
-// operands {G = [dq|dk|dv] 23x40 | T 23x20 | dctx 23x20 | X 23x4}; the V rows
+// operands {G = [dq|dk|dv] 23x40 | (unused 23x20) | dctx 23x20 | X 23x4}; the V rows
 // carry dctx in phase 3.  63 KB per workgroup: two workgroups (8 waves) per CU.
 constexpr int kBwdRows = 8;
 constexpr int kBwdThreads = 256;
 constexpr int kOffK = 0, kOffQ = 230, kOffV = 460, kOffP = 920, kOffS = 1449;  // attention phase
-constexpr int kOffG = 0, kOffT = 920, kOffD = 1380, kOffX = 1840;               // reduction phase
+constexpr int kOffG = 0, kOffD = 1380, kOffX = 1840;  // reduction phase
 constexpr int kSampleF = 1980;  // floats per sample (>= 1978 and >= 1932; multiple of 4)
 constexpr int kEFUnits = kTok * (kGd / 4);           // 345 (token, 4 rows of [g|dctx])
 

@@ -131,19 +131,30 @@ MM_HD DirWin gather_dir(const View& v, int x, int y, int ad) {
     const bool okl = (unsigned)(x - sx) < (unsigned)v.w && (unsigned)(y - sy) < (unsigned)v.h;
     const int step = dx + dy * v.w;
     const int offr = okr ? sx + sy * v.w : 0, offl = okl ? -(sx + sy * v.w) : 0;
-    const uint8_t* base = v.L + y * v.w + x;
+    const int base = y * v.w + x;
+    // all 13 cells are read unconditionally (clamped indices never leave the
+    // maze; a missing side row reads the ray cell itself) and combined with
+    // bitwise logic, so the reads issue back to back with no branches
+    int c[5], cr[4], cl[4];
+#pragma unroll
+    for (int j = 1; j <= 5; j++) {
+        const int idx = base + min(j, lim) * step;
+        c[j - 1] = v.L[idx] & 3;
+        if (j <= 4) {
+            cr[j - 1] = v.L[idx + offr] & 3;
+            cl[j - 1] = v.L[idx + offl] & 3;
+        }
+    }
     DirWin w{0, 0, 0, 0};
 #pragma unroll
     for (int j = 1; j <= 5; j++) {
-        const bool in = j <= lim;
-        const uint8_t* cp = base + min(j, lim) * step;  // clamped: never leaves the maze
-        const int c = cp[0] & 3;
-        w.fwd |= (uint32_t)(in && c != 1) << (j - 1);
+        const uint32_t in = j <= lim;
+        w.fwd |= (in & (uint32_t)(c[j - 1] != 1)) << (j - 1);
         if (j <= 4) {
-            w.m2 |= (uint32_t)(in && c == 2) << (j - 1);
-            w.m3 |= (uint32_t)(in && c == 3) << (j - 1);
-            const bool so = in && ((okr && (cp[offr] & 3) != 1) || (okl && (cp[offl] & 3) != 1));
-            w.side |= (uint32_t)so << (j - 1);
+            w.m2 |= (in & (uint32_t)(c[j - 1] == 2)) << (j - 1);
+            w.m3 |= (in & (uint32_t)(c[j - 1] == 3)) << (j - 1);
+            const uint32_t so = ((uint32_t)okr & (uint32_t)(cr[j - 1] != 1)) | ((uint32_t)okl & (uint32_t)(cl[j - 1] != 1));
+            w.side |= (in & so) << (j - 1);
         }
     }
     return w;
@@ -155,7 +166,8 @@ MM_HD int ray_hit(int x, int y, int ad, int tx, int ty, int L) {
     const int dx = ddx(ad), dy = ddy(ad);
     const int rx = tx - x, ry = ty - y;
     const int j = rx * dx + ry * dy;
-    return (rx == j * dx && ry == j * dy && j >= 1 && j <= L) ? j : 0;
+    // bitwise (not short-circuit) conditions: no divergent branches
+    return ((rx == j * dx) & (ry == j * dy) & (j >= 1) & (j <= L)) ? j : 0;
 }
 
 // Geometry of one relative direction d of an observation, packed in a word:
@@ -171,8 +183,9 @@ MM_HD uint32_t summarize_dir(const View& v, int x, int y, int dir, int d, int ta
     const int t = __builtin_ctz(~w.fwd);
     const int L = t < 4 ? t : 4;
     const int je = ray_hit(x, y, ad, v.ex, v.ey, L);
-    const int jk = (v.kx >= 0) ? ray_hit(x, y, ad, v.kx, v.ky, L) : 0;
-    const int ja = q_reg ? ray_hit(x, y, ad, qx, qy, L) : 0;
+    const int jk0 = ray_hit(x, y, ad, v.kx, v.ky, L), ja0 = ray_hit(x, y, ad, qx, qy, L);
+    const int jk = (v.kx >= 0) ? jk0 : 0;
+    const int ja = q_reg ? ja0 : 0;
     const uint32_t vis = (1u << L) - 1u;
     const int own = __builtin_popcount((tag == 2 ? w.m2 : w.m3) & vis);
     const int oth = __builtin_popcount((tag == 2 ? w.m3 : w.m2) & vis);
@@ -181,7 +194,7 @@ MM_HD uint32_t summarize_dir(const View& v, int x, int y, int dir, int d, int ta
     // a dead end at distance j.
     const uint32_t stop = (w.side | ~(w.fwd >> 1)) & 0xfu;
     const int j0 = __builtin_ctz(stop | 0x10u) + 1;  // 5: no stop within 4 cells
-    const int dead = !(w.fwd & 1u) ? 4 : ((j0 <= 4 && !(w.side >> (j0 - 1) & 1u)) ? 4 - j0 : 0);
+    const int dead = !(w.fwd & 1u) ? 4 : (((j0 <= 4) & !((w.side >> ((j0 - 1) & 31)) & 1u)) ? 4 - j0 : 0);
     return (uint32_t)L | (uint32_t)je << 3 | (uint32_t)jk << 6 | (uint32_t)ja << 9 | (uint32_t)own << 12 |
            (uint32_t)oth << 15 | (uint32_t)dead << 18;
 }

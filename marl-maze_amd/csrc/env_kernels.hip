@@ -342,12 +342,21 @@ __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __res
 // ---------------------------------------------------------------------------
 // step (one thread per maze)
 // ---------------------------------------------------------------------------
-// Four lanes per maze: lane q = 2a + h works on agent a's relative
-// directions 2h and 2h+1.  The cheap order-dependent work (moves, the replay
-// of both observations, reward) is done redundantly by all four lanes, so no
-// state has to be exchanged except the eight direction summaries (shuffles).
+// Four lanes per maze, two in each of the workgroup's two wavefronts: the
+// lane of agent a in wavefront h works on agent a's relative directions 2h
+// and 2h+1 and writes half h of agent a's observation row.  The cheap
+// order-dependent work (moves, the replay of both observations, reward) is
+// done redundantly by all four lanes, so only the eight direction summaries
+// are exchanged (through LDS).
 constexpr int kLanes = 4;
 constexpr int kMPB4 = 32;  // mazes per 128-thread workgroup
+
+// LDS of k_step: the workgroup's layouts, later overlaid by its staged obs and
+// mask rows, then the direction summaries (8 words per maze)
+__host__ __device__ inline int step_sum_off(int stride) {
+    const int lay = kMPB4 * stride, rows = kMPB4 * 2 * (kObs * 4 + kMask);
+    return ((lay > rows ? lay : rows) + 15) & ~15;
+}
 
 __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8_t* __restrict__ act,
                                                         float* __restrict__ obs, uint8_t* __restrict__ masks,
@@ -357,9 +366,14 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     const int stride = env.layout_stride;
     const int m0 = blockIdx.x * kMPB4;
     const int nb = min(kMPB4, env.n - m0);
-    const int lm = threadIdx.x >> 2;  // maze within the workgroup
-    const int q = threadIdx.x & 3;    // lane within the maze
-    const int a = q >> 1, h = q & 1;
+    // wavefront h (0, 1) works on relative directions 2h, 2h+1 of both agents
+    // and builds half h of their observation rows; lane l of a wavefront:
+    // maze l >> 1, agent l & 1.  h is wavefront-uniform, so each wavefront
+    // computes only its half of the observation.
+    const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lm = (threadIdx.x & 63) >> 1;  // maze within the workgroup
+    const int a = threadIdx.x & 1;
+    const bool lead = h == 0 && a == 0;  // writes the maze's marks and state to HBM
     const int m = m0 + lm;
     const bool valid = lm < nb;
 #ifdef MM_STEP_STAMPS  // tools/step_stamps.py: per-workgroup phase clocks into work[64 + 12*block]
@@ -390,34 +404,37 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     Agent a0 = load_agent(g0, 2);
     Agent a1 = load_agent(g1, 3);
     uint32_t status = mz.status;
-    float o[kObs];
-    uint8_t mk[kMask];
     int first_key = 0, have_key = 0;
     if (valid) {
-        uint8_t* gl = (q == 0) ? env.layout + (size_t)m * stride : nullptr;
-        // maze.py:75-90 (the four lanes write identical mark bytes into LDS)
+        // maze.py:75-90: both wavefronts replay the moves and write the same
+        // mark bytes into LDS; the lead lane also writes them to HBM
+        uint8_t* gl = lead ? env.layout + (size_t)m * stride : nullptr;
         mz.t += 1;
         v.t = mz.t;
         first_key = agent_step(v, a0, ac.x, ac.y, gl, status);
         const int have_key0 = a0.f(MM_AF_HAS_KEY);
         first_key += agent_step(v, a1, ac.z, ac.w, gl, status);
         have_key = have_key0 + a1.f(MM_AF_HAS_KEY);
-        MM_STAMP(5);
-        // geometry of this lane's two directions of agent a
+    }
+    // the other wavefront's writes of the same mark bytes (possibly
+    // interleaved with ours) are done before any ray reads the marks
+    __syncthreads();
+    MM_STAMP(5);
+    // direction summaries of the maze, [agent][relative direction]
+    uint32_t* ssum = reinterpret_cast<uint32_t*>(smem + step_sum_off(stride)) + 8 * lm;
+    if (valid) {  // geometry of this lane's two directions of agent a
         const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
         const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
         const uint32_t sB = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + 1, me0.tag, ot0.x, ot0.y, true);
-        const int base = (threadIdx.x & 63) & ~3;
-        uint32_t sum0[4], sum1[4];
-        sum0[0] = __shfl(sA, base + 0);
-        sum0[1] = __shfl(sB, base + 0);
-        sum0[2] = __shfl(sA, base + 1);
-        sum0[3] = __shfl(sB, base + 1);
-        sum1[0] = __shfl(sA, base + 2);
-        sum1[1] = __shfl(sB, base + 2);
-        sum1[2] = __shfl(sA, base + 3);
-        sum1[3] = __shfl(sB, base + 3);
-        MM_STAMP(6);
+        *reinterpret_cast<uint2*>(ssum + 4 * a + 2 * h) = make_uint2(sA, sB);
+    }
+    __syncthreads();
+    MM_STAMP(6);
+    float oh[33];  // this wavefront's half of the observation row
+    uint8_t mk[kMask];
+    if (valid) {
+        const uint4 s0 = *reinterpret_cast<const uint4*>(ssum), s1 = *reinterpret_cast<const uint4*>(ssum + 4);
+        const uint32_t sum0[4] = {s0.x, s0.y, s0.z, s0.w}, sum1[4] = {s1.x, s1.y, s1.z, s1.w};
         // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1
         const Vis r0 = replay(v, a0, a1, sum0);
         const Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
@@ -430,15 +447,26 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
         uint32_t sm[4];
 #pragma unroll
         for (int d = 0; d < 4; d++) sm[d] = a ? sum1[d] : sum0[d];
-        const int am = build_obs(v, me, rm, sm, o, mk);
-        if (exit_ready) {  // maze.py:107-113
-            if (!v.is_end(me.x, me.y)) {
+        float o[kObs];
+        if (h == 0) {  // elements [0, 33) and the action mask
+            const int am = build_obs(v, me, rm, sm, o, mk);
+            if (exit_ready) {  // maze.py:107-113
+                if (!v.is_end(me.x, me.y)) {
 #pragma unroll
-                for (int d = 0; d < 4; d++) mk[d] = (uint8_t)(d == am);
-            } else {
-                mk[0] = mk[1] = mk[2] = mk[3] = 0;
-                mk[4] = 1;
+                    for (int d = 0; d < 4; d++) mk[d] = (uint8_t)(d == am);
+                } else {
+                    mk[0] = mk[1] = mk[2] = mk[3] = 0;
+                    mk[4] = 1;
+                }
             }
+#pragma unroll
+            for (int k = 0; k < 33; k++) oh[k] = o[k];
+        } else {  // elements [33, 65); the compiler drops the rest of build_obs
+            uint8_t unused[kMask];
+            build_obs(v, me, rm, sm, o, unused);
+#pragma unroll
+            for (int k = 0; k < 32; k++) oh[k] = o[33 + k];
+            oh[32] = 0.f;
         }
     }
     MM_STAMP(2);
@@ -449,12 +477,10 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     float* sobs = reinterpret_cast<float*>(smem);
     uint8_t* smk = smem + kMPB4 * 2 * kObs * 4;
     if (valid) {
-        float* orow = sobs + (2 * lm + a) * kObs + 33 * h;  // lane h: elements [33h, 33h + 33 - h)
+        float* orow = sobs + (2 * lm + a) * kObs + 33 * h;  // wavefront h: elements [33h, 33h + 33 - h)
 #pragma unroll
-        for (int k = 0; k < 33; k++) {
-            const float val = h ? (k < 32 ? o[33 + k] : 0.f) : o[k];
-            if (k < 32 || h == 0) orow[k] = val;
-        }
+        for (int k = 0; k < 33; k++)
+            if (k < 32 || h == 0) orow[k] = oh[k];
         if (h == 0) {
 #pragma unroll
             for (int i = 0; i < kMask; i++) smk[(2 * lm + a) * kMask + i] = mk[i];
@@ -476,7 +502,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
         w[8] = (int32_t)(st[7] - st[6]);  // replays
     }
 #endif
-    if (!valid || q != 0) return;
+    if (!valid || !lead) return;
     // reward / done (maze.py:115-121) and state write-back
     float r = first_key ? 0.5f * first_key : 0.f;
     uint8_t dn = 0;
@@ -507,10 +533,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     env.agents[2 * m + 1] = pack_agent(a1);
 }
 
-inline size_t step_lds_bytes(int stride) {
-    const int lay = kMPB4 * stride, rows = kMPB4 * 2 * (kObs * 4 + kMask);
-    return (size_t)(((lay > rows ? lay : rows) + 15) & ~15);
-}
+inline size_t step_lds_bytes(int stride) { return (size_t)step_sum_off(stride) + kMPB4 * 8 * 4; }
 
 inline int check_env(const mm_env_t* env) {
     if (!env || env->n <= 0 || !env->layout || !env->agents || !env->mazes || !env->rng || !env->work) return MM_E_ARG;
