@@ -42,12 +42,17 @@ __device__ __forceinline__ void copy_in(uint8_t* dst, const uint8_t* src, int by
     for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) dst[k] = src[k];
 }
 
+// Non-temporal (streaming) stores: the rows go out to memory while other
+// workgroups still compute, instead of collecting as dirty L2 lines that the
+// end-of-kernel release has to write back (k_step writes ~41 MB per launch at
+// 65,536 mazes, more than the 32 MB of L2).
 __device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int bytes) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const int nv = bytes >> 4;
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
-    for (int k = threadIdx.x; k < nv; k += blockDim.x) d4[k] = s4[k];
-    for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) dst[k] = src[k];
+    const u32x4* s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4* d4 = reinterpret_cast<u32x4*>(dst);
+    for (int k = threadIdx.x; k < nv; k += blockDim.x) __builtin_nontemporal_store(s4[k], d4 + k);
+    for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) __builtin_nontemporal_store(src[k], dst + k);
 }
 
 // ---------------------------------------------------------------------------
@@ -357,6 +362,31 @@ __host__ __device__ inline int step_sum_off(int stride) {
     const int lay = kMPB4 * stride, rows = kMPB4 * 2 * (kObs * 4 + kMask);
     return ((lay > rows ? lay : rows) + 15) & ~15;
 }
+constexpr int kXchgBytes = kMPB4 * 2 * 64;  // two replay records per maze
+// replay records: in the gap between the layouts and the end of the obs
+// staging area when it is large enough (10x10 mazes: 5.4 KB), else after the
+// summaries -- either way they are dead before the rows are staged
+__host__ __device__ inline int step_xchg_off(int stride) {
+    const int lay = (kMPB4 * stride + 15) & ~15, rows = kMPB4 * 2 * (kObs * 4 + kMask);
+    return lay + kXchgBytes <= rows ? lay : step_sum_off(stride) + kMPB4 * 8 * 4;
+}
+
+// Replay hand-off record (4 x int4): the replayed agent's fields that
+// replay() changes, the other agent's flags, and the ray visibility masks.
+__device__ __forceinline__ void put_replay(int4* r, const Agent& s, int qflags, const Vis& vis) {
+    r[0] = make_int4(s.flags, s.tfls, s.olsx, s.olsy);
+    r[1] = make_int4(s.exit_len, s.minx, s.maxx, s.miny);
+    r[2] = make_int4(s.maxy, qflags, vis.va, vis.vk);
+    r[3] = make_int4(vis.vad, 0, 0, 0);
+}
+
+__device__ __forceinline__ void get_replay(const int4* r, Agent& s, int& qflags, Vis& vis) {
+    const int4 w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3];
+    s.flags = w0.x; s.tfls = w0.y; s.olsx = w0.z; s.olsy = w0.w;
+    s.exit_len = w1.x; s.minx = w1.y; s.maxx = w1.z; s.miny = w1.w;
+    s.maxy = w2.x; qflags = w2.y; vis.va = w2.z; vis.vk = w2.w;
+    vis.vad = w3.x;
+}
 
 __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8_t* __restrict__ act,
                                                         float* __restrict__ obs, uint8_t* __restrict__ masks,
@@ -430,18 +460,44 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     }
     __syncthreads();
     MM_STAMP(6);
+    uint32_t sum0[4], sum1[4];
+    if (valid) {
+        const uint4 s0 = *reinterpret_cast<const uint4*>(ssum), s1 = *reinterpret_cast<const uint4*>(ssum + 4);
+        sum0[0] = s0.x; sum0[1] = s0.y; sum0[2] = s0.z; sum0[3] = s0.w;
+        sum1[0] = s1.x; sum1[1] = s1.y; sum1[2] = s1.z; sum1[3] = s1.w;
+    }
+    // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1.
+    // The two replays form a chain: wavefront 0 replays agent 0, wavefront 1
+    // then replays agent 1, and each hands its result to the other through
+    // LDS (one record per replay and maze), so every replay runs once.
+    int4* xrec = reinterpret_cast<int4*>(smem + step_xchg_off(stride)) + 8 * lm;  // [replay][4 x int4]
+    Vis r0{0, 0, 0}, r1{0, 0, 0};
+    if (valid && h == 0) {
+        r0 = replay(v, a0, a1, sum0);
+        if (a == 0) put_replay(xrec, a0, a1.flags, r0);
+    }
+    __syncthreads();
+    Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
+    if (valid && h == 1) {
+        int f1 = a1.flags;
+        get_replay(xrec, a0, f1, r0);
+        a1.flags = f1;
+        a0_obs = a0;
+        r1 = replay(v, a1, a0, sum1);
+        if (a == 0) put_replay(xrec + 4, a1, a0.flags, r1);
+    }
+    __syncthreads();
+    if (valid && h == 0) {
+        int f0 = a0.flags;
+        get_replay(xrec + 4, a1, f0, r1);
+        a0.flags = f0;
+    }
+    const bool exit_ready = a0_obs.f(MM_AF_TEAM_KEY) && a0_obs.f(MM_AF_KNOWS_END) && a1.f(MM_AF_TEAM_KEY) &&
+                            a1.f(MM_AF_KNOWS_END);
+    MM_STAMP(7);
     float oh[33];  // this wavefront's half of the observation row
     uint8_t mk[kMask];
     if (valid) {
-        const uint4 s0 = *reinterpret_cast<const uint4*>(ssum), s1 = *reinterpret_cast<const uint4*>(ssum + 4);
-        const uint32_t sum0[4] = {s0.x, s0.y, s0.z, s0.w}, sum1[4] = {s1.x, s1.y, s1.z, s1.w};
-        // maze.py:99-106: agent 0 observes (may update agent 1), then agent 1
-        const Vis r0 = replay(v, a0, a1, sum0);
-        const Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
-        const bool ready0 = a0.f(MM_AF_TEAM_KEY) && a0.f(MM_AF_KNOWS_END);
-        const Vis r1 = replay(v, a1, a0, sum1);
-        const bool exit_ready = ready0 && a1.f(MM_AF_TEAM_KEY) && a1.f(MM_AF_KNOWS_END);
-        MM_STAMP(7);
         const Agent me = a ? a1 : a0_obs;
         const Vis rm = a ? r1 : r0;
         uint32_t sm[4];
@@ -533,7 +589,11 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     env.agents[2 * m + 1] = pack_agent(a1);
 }
 
-inline size_t step_lds_bytes(int stride) { return (size_t)step_sum_off(stride) + kMPB4 * 8 * 4; }
+inline size_t step_lds_bytes(int stride) {
+    const size_t sums_end = (size_t)step_sum_off(stride) + kMPB4 * 8 * 4;
+    const size_t xchg_end = (size_t)step_xchg_off(stride) + kXchgBytes;
+    return sums_end > xchg_end ? sums_end : xchg_end;
+}
 
 inline int check_env(const mm_env_t* env) {
     if (!env || env->n <= 0 || !env->layout || !env->agents || !env->mazes || !env->rng || !env->work) return MM_E_ARG;
