@@ -55,6 +55,17 @@ __device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* src, int b
     for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) __builtin_nontemporal_store(src[k], dst + k);
 }
 
+// one 32-byte state record (mm_maze_t / mm_agent_t) as two streaming 16-byte stores
+template <class T>
+__device__ __forceinline__ void store_nt32(T* dst, const T& v) {
+    static_assert(sizeof(T) == 32, "32-byte records");
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w[2];
+    __builtin_memcpy(w, &v, 32);
+    __builtin_nontemporal_store(w[0], reinterpret_cast<u32x4*>(dst));
+    __builtin_nontemporal_store(w[1], reinterpret_cast<u32x4*>(dst) + 1);
+}
+
 // ---------------------------------------------------------------------------
 // seed
 // ---------------------------------------------------------------------------
@@ -568,8 +579,8 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     } else if (mz.t >= env.max_timestep) {
         dn = 1;
     }
-    reward[m] = r;
-    done[m] = dn;
+    __builtin_nontemporal_store(r, reward + m);
+    __builtin_nontemporal_store(dn, done + m);
     if (ep_stats)  // (episode length, shortest_path_len) of an episode that ended here (PPO.py:129,131)
         reinterpret_cast<int2*>(ep_stats)[m] = dn ? make_int2(mz.t, mz.path_len) : make_int2(0, 0);
     mz.kx = (int8_t)v.kx;
@@ -584,9 +595,9 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
             if (pos < env.n) env.work[kListOff + pos] = m;  // (queue not drained by the caller: ignore)
         }
     }
-    env.mazes[m] = mz;
-    env.agents[2 * m] = pack_agent(a0);
-    env.agents[2 * m + 1] = pack_agent(a1);
+    store_nt32(env.mazes + m, mz);
+    store_nt32(env.agents + 2 * m, pack_agent(a0));
+    store_nt32(env.agents + 2 * m + 1, pack_agent(a1));
 }
 
 inline size_t step_lds_bytes(int stride) {
