@@ -218,6 +218,11 @@ int mm_ppo_loss(const float* heads, const uint8_t* masks, const int8_t* actions,
 int mm_ppo_loss_bwd(const float* heads, const uint8_t* masks, const int8_t* actions, const float* coef,
                     const float* dloss, int M, float* dheads, void* stream);
 
+/* Split-K weight gradients (the Linear backward dW = dY^T X over >= 65,536
+ * rows, networks.py:35-41 / :87-106 under autograd): out [n] = sum over s of
+ * x [S, n] (s ascending) + addend [n] (addend may be NULL; out may alias it). */
+int mm_sum_leading(const float* x, int S, long n, const float* addend, float* out, void* stream);
+
 /* The actor's two heads fused with mm_sample: logits =
  * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]
  * [6, K] and b [6] (networks.py:38-41), then the draw of mm_sample with the

@@ -36,7 +36,8 @@ EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
-           "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd")
+           "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
+           "mm_sum_leading")
 
 
 class EnvDesc(ctypes.Structure):
@@ -103,6 +104,8 @@ def lib():
         L.mm_ppo_loss.restype = i32
         L.mm_ppo_loss_bwd.argtypes = [P, P, P, P, P, i32, P, P]
         L.mm_ppo_loss_bwd.restype = i32
+        L.mm_sum_leading.argtypes = [P, i32, ctypes.c_long, P, P, P]
+        L.mm_sum_leading.restype = i32
         L.mm_x3_mbits_len.argtypes = [i32]
         L.mm_x3_mbits_len.restype = ctypes.c_long
         L.mm_x3_nt_f32a.restype = i32

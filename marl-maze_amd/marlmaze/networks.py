@@ -180,10 +180,18 @@ def _split_k_wgrad(dy, x):
     if S == 1:
         return dy.t().mm(x)
     m = M - M % S
-    dw = torch.bmm(dy[:m].view(S, m // S, -1).transpose(1, 2), x[:m].view(S, m // S, -1)).sum(0)
-    if m < M:
-        dw = dw + dy[m:].t().mm(x[m:])
-    return dw
+    part = torch.bmm(dy[:m].view(S, m // S, -1).transpose(1, 2), x[:m].view(S, m // S, -1))
+    rest = dy[m:].t().mm(x[m:]) if m < M else None
+    if not part.is_cuda:
+        return part.sum(0) if rest is None else part.sum(0) + rest
+    from . import _lib
+
+    # the S partials and the remainder rows' product summed in one pass (mm_sum_leading)
+    out = rest if rest is not None else torch.empty(part.shape[1:], dtype=part.dtype, device=part.device)
+    _lib.check(_lib.lib().mm_sum_leading(_lib.ptr(part), S, part[0].numel(),
+                                         _lib.ptr(rest) if rest is not None else None, _lib.ptr(out),
+                                         _lib.stream_ptr()), "mm_sum_leading")
+    return out
 
 
 def _x3_trunk_fwd(h0, ws, bs, need_bits):

@@ -369,3 +369,19 @@ def test_fused_policy_loss_matches_torch(M):
     got, = torch.autograd.grad(loss, z2)
     assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item()) + 1e-7, (loss.item(), ref.item())
     assert (got - gref).abs().max().item() <= 1e-6 * gref.abs().max().item() + 1e-9
+
+
+@pytest.mark.parametrize("M,N,K", [(419430, 264, 460), (16 * 4096, 6, 264), (70001, 7, 13)])
+def test_split_k_wgrad_matches_fp64(M, N, K):
+    """networks._split_k_wgrad (batched split-K GEMM + mm_sum_leading, incl. the
+    remainder rows and the unaligned scalar path) against an fp64 dY^T X."""
+    from marlmaze.networks import _split_k_wgrad
+
+    g = torch.Generator(device="cuda").manual_seed(M)
+    dy = torch.randn(M, N, device="cuda", generator=g)
+    x = torch.randn(M, K, device="cuda", generator=g)
+    dw = _split_k_wgrad(dy, x)
+    ref = dy.double().t().mm(x.double())
+    scale = dy.double().abs().t().mm(x.double().abs())
+    err = ((dw.double() - ref).abs() / scale).max().item()
+    assert dw.shape == (N, K) and err < 1e-5, err
