@@ -34,11 +34,19 @@ constexpr int kListOff = 64;        // done list starts at work[64]
 // ---------------------------------------------------------------------------
 // cooperative contiguous copies (whole workgroup)
 // ---------------------------------------------------------------------------
+// HBM -> LDS by LDS-DMA (16 bytes per lane, lane-linear): every piece is in
+// flight at once and the copy waits once, at the caller's barrier (a
+// register round trip per piece waited one HBM latency per loop iteration).
+// src and dst 16-byte aligned.
 __device__ __forceinline__ void copy_in(uint8_t* dst, const uint8_t* src, int bytes) {
     const int nv = bytes >> 4;
+    const int lane = threadIdx.x & 63;
+    const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
     const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
-    for (int k = threadIdx.x; k < nv; k += blockDim.x) d4[k] = s4[k];
+    for (int k0 = 0; k0 < nv; k0 += blockDim.x) {
+        if (k0 + wbase + lane < nv)
+            __builtin_amdgcn_global_load_lds(s4 + k0 + wbase + lane, dst + 16 * (k0 + wbase), 16, 0, 0);
+    }
     for (int k = (nv << 4) + threadIdx.x; k < bytes; k += blockDim.x) dst[k] = src[k];
 }
 
@@ -425,7 +433,9 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
 #else
 #define MM_STAMP(i)
 #endif
-    // per-maze state loads are issued before the layout staging barrier
+    // the layout DMA is issued first, then the per-maze state loads; all of
+    // them are in flight together until the staging barrier
+    copy_in(smem, env.layout + (size_t)m0 * stride, nb * stride);
     mm_maze_t mz{};
     mm_agent_t g0{}, g1{};
     char4 ac{};
@@ -435,7 +445,6 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
         g1 = env.agents[2 * m + 1];
         ac = reinterpret_cast<const char4*>(act)[m];
     }
-    copy_in(smem, env.layout + (size_t)m0 * stride, nb * stride);
     __syncthreads();
     MM_STAMP(1);
     View v;
