@@ -235,15 +235,26 @@ constexpr int kFwdRows = 8;  // samples per iteration of a 256-thread workgroup
 constexpr int kTabF = kQkv * kPin + kQkv + kEmb * kPin + kEmb;  // 300 floats per token: A | c | Wp | bp
 // (300 dwords = 75 16-byte quads, odd: a wave's per-token 16-byte reads are bank-conflict free)
 
+// all of a thread's table loads are issued before its LDS writes (one L2
+// round trip per workgroup instead of one per element); 256 threads
 __device__ __forceinline__ void stage_tables(const float* __restrict__ ws, float* tab) {
-    for (int e = threadIdx.x; e < kTok * kTabF; e += blockDim.x) {
+    constexpr int kN = kTok * kTabF, kPer = (kN + 255) / 256;
+    float v[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int e = threadIdx.x + 256 * u;
         const int i = e / kTabF, f = e % kTabF;
-        float v;
-        if (f < kQkv * kPin) v = ws[kWsA + i * kQkv * kPin + f];
-        else if (f < kQkv * kPin + kQkv) v = ws[kWsC + i * kQkv + f - kQkv * kPin];
-        else if (f < kQkv * kPin + kQkv + kEmb * kPin) v = ws[kWsWP + i * kEmb * kPin + f - kQkv * (kPin + 1)];
-        else v = ws[kWsBP + i * kEmb + f - kQkv * (kPin + 1) - kEmb * kPin];
-        tab[e] = v;
+        int src;
+        if (f < kQkv * kPin) src = kWsA + i * kQkv * kPin + f;
+        else if (f < kQkv * kPin + kQkv) src = kWsC + i * kQkv + f - kQkv * kPin;
+        else if (f < kQkv * kPin + kQkv + kEmb * kPin) src = kWsWP + i * kEmb * kPin + f - kQkv * (kPin + 1);
+        else src = kWsBP + i * kEmb + f - kQkv * (kPin + 1) - kEmb * kPin;
+        v[u] = e < kN ? ws[src] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int e = threadIdx.x + 256 * u;
+        if (e < kN) tab[e] = v[u];
     }
 }
 

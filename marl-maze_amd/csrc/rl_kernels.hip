@@ -180,7 +180,21 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* 
                                                                    float* __restrict__ joint,
                                                                    float* __restrict__ logits) {
     __shared__ __attribute__((aligned(16))) float W[6 * kHsMaxK];
-    for (int e = threadIdx.x; e < 6 * K; e += blockDim.x) W[e] = w[e];
+    // loads batched ahead of the LDS writes: one L2 round trip, not one per element
+    constexpr int kB = 8;
+    for (int e0 = threadIdx.x; e0 < 6 * K; e0 += kB * blockDim.x) {
+        float t[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int e = e0 + u * blockDim.x;
+            t[u] = e < 6 * K ? w[e] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int e = e0 + u * blockDim.x;
+            if (e < 6 * K) W[e] = t[u];
+        }
+    }
     __syncthreads();
     const int j = threadIdx.x % kHsLanes;
     const int row = blockIdx.x * kHsRows + threadIdx.x / kHsLanes;

@@ -422,9 +422,19 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz,
                                                    const uint32_t* __restrict__ bits, int M, int N,
                                                    float* __restrict__ dy, float* __restrict__ colsum) {
     __shared__ float sw[kHeadsMaxJ][16 * NT];
-    for (int e = threadIdx.x; e < kHeadsMaxJ * 16 * NT; e += blockDim.x) {
-        const int j = e / (16 * NT), n = e % (16 * NT);
-        sw[j][n] = (j < J && n < N) ? W[(size_t)j * N + n] : 0.f;
+    {  // loads batched ahead of the LDS writes (one L2 round trip per workgroup); 256 threads
+        constexpr int kN = kHeadsMaxJ * 16 * NT, kPer = (kN + 255) / 256;
+        float t[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            const int e = threadIdx.x + 256 * u, j = e / (16 * NT), n = e % (16 * NT);
+            t[u] = (e < kN && j < J && n < N) ? W[(size_t)j * N + n] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            const int e = threadIdx.x + 256 * u;
+            if (e < kN) sw[e / (16 * NT)][e % (16 * NT)] = t[u];
+        }
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
