@@ -100,7 +100,7 @@ typedef struct {
     int32_t rand_sizes;            /* maze.py:23 */
     int32_t rand_lo, rand_hi;      /* rand_range */
     int32_t layout_stride;         /* bytes per maze layout (>= side_max^2) */
-    uint8_t* layout;               /* [n, layout_stride] */
+    uint8_t* layout;               /* [n, layout_stride], 16-byte aligned (as agents, mazes) */
     mm_agent_t* agents;            /* [n, 2] */
     mm_maze_t* mazes;              /* [n] */
     uint32_t* rng;                 /* [n, MM_RNG_WORDS] */

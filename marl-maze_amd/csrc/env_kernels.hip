@@ -621,6 +621,10 @@ inline int check_env(const mm_env_t* env) {
     if (need < 0 || env->size_w < 2 || env->size_h < 2) return MM_E_SIZE;
     if (env->rand_sizes && (env->rand_lo < 2 || env->rand_hi < env->rand_lo)) return MM_E_SIZE;
     if (env->layout_stride < need) return MM_E_SIZE;
+    // k_step stages the layouts by 16-byte LDS-DMA; the state records are 32-byte structs
+    if ((reinterpret_cast<uintptr_t>(env->layout) | reinterpret_cast<uintptr_t>(env->agents) |
+         reinterpret_cast<uintptr_t>(env->mazes)) & 15)
+        return MM_E_ARG;
     if (env->difficulty < 1 || env->max_timestep < 1) return MM_E_ARG;
     return 0;
 }
