@@ -47,7 +47,7 @@ extern "C" {
 #define MM_MASK_DIM 6
 #define MM_RNG_WORDS 625   /* CPython random.getstate()[1]: 624 words + index */
 #define MM_MAX_SIDE 41     /* layout side limit (default_size <= 21) */
-#define MM_MAZES_PER_BLOCK 32  /* mazes per env-step workgroup (4 lanes each) */
+#define MM_MAZES_PER_BLOCK 32  /* mazes per env-step workgroup (4 lanes each); 16 when layout_stride > 1024 */
 
 #define MM_E_ARG (-1)
 #define MM_E_SIZE (-2)

@@ -368,26 +368,31 @@ __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __res
 // ---------------------------------------------------------------------------
 // Four lanes per maze, two in each of the workgroup's two wavefronts: the
 // lane of agent a in wavefront h works on agent a's relative directions 2h
-// and 2h+1 and writes half h of agent a's observation row.  The cheap
-// order-dependent work (moves, the replay of both observations, reward) is
-// done redundantly by all four lanes, so only the eight direction summaries
-// are exchanged (through LDS).
-constexpr int kLanes = 4;
-constexpr int kMPB4 = 32;  // mazes per 128-thread workgroup
+// and 2h+1 and writes half h of agent a's observation row.  The moves and
+// the reward are computed redundantly by all four lanes; the eight direction
+// summaries and the two chained replays' results are exchanged through LDS.
+constexpr int kStepThreads = 128;  // two wavefronts
+// mazes per workgroup: 32 (two lanes of each wavefront per maze), or 16 for
+// layouts over 1 KB (the upper half of each wavefront idles; the workgroup's
+// LDS halves, so twice as many workgroups share a CU)
+constexpr int kMPBig = 16, kMPBigStride = 1024;
 
 // LDS of k_step: the workgroup's layouts, later overlaid by its staged obs and
 // mask rows, then the direction summaries (8 words per maze)
+template <int MPB>
 __host__ __device__ inline int step_sum_off(int stride) {
-    const int lay = kMPB4 * stride, rows = kMPB4 * 2 * (kObs * 4 + kMask);
+    const int lay = MPB * stride, rows = MPB * 2 * (kObs * 4 + kMask);
     return ((lay > rows ? lay : rows) + 15) & ~15;
 }
-constexpr int kXchgBytes = kMPB4 * 2 * 64;  // two replay records per maze
+template <int MPB>
+constexpr int xchg_bytes() { return MPB * 2 * 64; }  // two replay records per maze
 // replay records: in the gap between the layouts and the end of the obs
 // staging area when it is large enough (10x10 mazes: 5.4 KB), else after the
 // summaries -- either way they are dead before the rows are staged
+template <int MPB>
 __host__ __device__ inline int step_xchg_off(int stride) {
-    const int lay = (kMPB4 * stride + 15) & ~15, rows = kMPB4 * 2 * (kObs * 4 + kMask);
-    return lay + kXchgBytes <= rows ? lay : step_sum_off(stride) + kMPB4 * 8 * 4;
+    const int lay = (MPB * stride + 15) & ~15, rows = MPB * 2 * (kObs * 4 + kMask);
+    return lay + xchg_bytes<MPB>() <= rows ? lay : step_sum_off<MPB>(stride) + MPB * 8 * 4;
 }
 
 // Replay hand-off record (4 x int4): the replayed agent's fields that
@@ -407,14 +412,15 @@ __device__ __forceinline__ void get_replay(const int4* r, Agent& s, int& qflags,
     vis.vad = w3.x;
 }
 
-__global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8_t* __restrict__ act,
+template <int MPB>
+__global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_t* __restrict__ act,
                                                         float* __restrict__ obs, uint8_t* __restrict__ masks,
                                                         float* __restrict__ reward, uint8_t* __restrict__ done,
                                                         int32_t* __restrict__ ep_stats, int list_done) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int stride = env.layout_stride;
-    const int m0 = blockIdx.x * kMPB4;
-    const int nb = min(kMPB4, env.n - m0);
+    const int m0 = blockIdx.x * MPB;
+    const int nb = min(MPB, env.n - m0);
     // wavefront h (0, 1) works on relative directions 2h, 2h+1 of both agents
     // and builds half h of their observation rows; lane l of a wavefront:
     // maze l >> 1, agent l & 1.  h is wavefront-uniform, so each wavefront
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     __syncthreads();
     MM_STAMP(5);
     // direction summaries of the maze, [agent][relative direction]
-    uint32_t* ssum = reinterpret_cast<uint32_t*>(smem + step_sum_off(stride)) + 8 * lm;
+    uint32_t* ssum = reinterpret_cast<uint32_t*>(smem + step_sum_off<MPB>(stride)) + 8 * lm;
     if (valid) {  // geometry of this lane's two directions of agent a
         const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
         const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
@@ -490,7 +496,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     // The two replays form a chain: wavefront 0 replays agent 0, wavefront 1
     // then replays agent 1, and each hands its result to the other through
     // LDS (one record per replay and maze), so every replay runs once.
-    int4* xrec = reinterpret_cast<int4*>(smem + step_xchg_off(stride)) + 8 * lm;  // [replay][4 x int4]
+    int4* xrec = reinterpret_cast<int4*>(smem + step_xchg_off<MPB>(stride)) + 8 * lm;  // [replay][4 x int4]
     Vis r0{0, 0, 0}, r1{0, 0, 0};
     if (valid && h == 0) {
         r0 = replay(v, a0, a1, sum0);
@@ -551,7 +557,7 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     // and store them with 16-byte coalesced writes.
     __syncthreads();
     float* sobs = reinterpret_cast<float*>(smem);
-    uint8_t* smk = smem + kMPB4 * 2 * kObs * 4;
+    uint8_t* smk = smem + MPB * 2 * kObs * 4;
     if (valid) {
         float* orow = sobs + (2 * lm + a) * kObs + 33 * h;  // wavefront h: elements [33h, 33h + 33 - h)
 #pragma unroll
@@ -609,9 +615,10 @@ __global__ __launch_bounds__(kMPB4* kLanes) void k_step(mm_env_t env, const int8
     store_nt32(env.agents + 2 * m + 1, pack_agent(a1));
 }
 
+template <int MPB>
 inline size_t step_lds_bytes(int stride) {
-    const size_t sums_end = (size_t)step_sum_off(stride) + kMPB4 * 8 * 4;
-    const size_t xchg_end = (size_t)step_xchg_off(stride) + kXchgBytes;
+    const size_t sums_end = (size_t)step_sum_off<MPB>(stride) + MPB * 8 * 4;
+    const size_t xchg_end = (size_t)step_xchg_off<MPB>(stride) + xchg_bytes<MPB>();
     return sums_end > xchg_end ? sums_end : xchg_end;
 }
 
@@ -677,12 +684,18 @@ extern "C" int mm_env_step_timed(const mm_env_t* env, const int8_t* actions, flo
     if (!actions || !obs || !masks || !reward || !done) return MM_E_ARG;
     if (auto_reset < 0 || auto_reset > 2) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
-    const size_t lds = step_lds_bytes(env->layout_stride);
-    const int grid = (env->n + kMPB4 - 1) / kMPB4;
     // hipExtLaunchKernel stamps the events at the kernel's own start / end
-    hipExtLaunchKernelGGL(k_step, dim3(grid), dim3(kMPB4 * kLanes), (uint32_t)lds, s, (hipEvent_t)ev_start,
-                          (hipEvent_t)ev_stop, 0, *env, actions, obs, masks, reward, done, ep_stats,
-                          auto_reset ? 1 : 0);
+    if (env->layout_stride > kMPBigStride) {
+        const size_t lds = step_lds_bytes<kMPBig>(env->layout_stride);
+        hipExtLaunchKernelGGL(k_step<kMPBig>, dim3((env->n + kMPBig - 1) / kMPBig), dim3(kStepThreads),
+                              (uint32_t)lds, s, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, *env, actions, obs,
+                              masks, reward, done, ep_stats, auto_reset ? 1 : 0);
+    } else {
+        const size_t lds = step_lds_bytes<2 * kMPBig>(env->layout_stride);
+        hipExtLaunchKernelGGL(k_step<2 * kMPBig>, dim3((env->n + 2 * kMPBig - 1) / (2 * kMPBig)),
+                              dim3(kStepThreads), (uint32_t)lds, s, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0,
+                              *env, actions, obs, masks, reward, done, ep_stats, auto_reset ? 1 : 0);
+    }
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
     if (auto_reset == 1) return launch_reset(env, nullptr, 1, obs, masks, s);
