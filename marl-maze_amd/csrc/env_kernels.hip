@@ -269,7 +269,15 @@ __device__ bool generate(const mm_env_t& env, GenLds& g, WaveRng& rng, int& w, i
 __device__ void generate_one(const mm_env_t& env, GenLds& g, int m) {
     const int lane = threadIdx.x;
     uint32_t* rs = env.rng + (size_t)m * MM_RNG_WORDS;
-    for (int k = lane; k < kMtN; k += 64) g.mt[k] = rs[k];
+    {  // the 624 state words: all loads in flight before the LDS writes
+        constexpr int kPer = (kMtN + 63) / 64;
+        uint32_t t[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; u++) t[u] = lane + 64 * u < kMtN ? rs[lane + 64 * u] : 0u;
+#pragma unroll
+        for (int u = 0; u < kPer; u++)
+            if (lane + 64 * u < kMtN) g.mt[lane + 64 * u] = t[u];
+    }
     WaveRng rng;
     rng.mt = g.mt;
     rng.idx = (int)rs[kMtN];
