@@ -136,9 +136,10 @@ MM_HD DirWin gather_dir(const View& v, int x, int y, int ad) {
     // maze; a missing side row reads the ray cell itself) and combined with
     // bitwise logic, so the reads issue back to back with no branches
     int c[5], cr[4], cl[4];
+    int idx = base;
 #pragma unroll
     for (int j = 1; j <= 5; j++) {
-        const int idx = base + min(j, lim) * step;
+        idx += j <= lim ? step : 0;  // base + min(j, lim) * step, without multiplies
         c[j - 1] = v.L[idx] & 3;
         if (j <= 4) {
             cr[j - 1] = v.L[idx + offr] & 3;
@@ -163,11 +164,15 @@ MM_HD DirWin gather_dir(const View& v, int x, int y, int ad) {
 // Distance j (1..L) at which the ray from (x, y) in absolute direction ad
 // passes (tx, ty); 0 if it does not within the L visible cells.
 MM_HD int ray_hit(int x, int y, int ad, int tx, int ty, int L) {
-    const int dx = ddx(ad), dy = ddy(ad);
+    // ad 1 (E, +x) and 3 (W, -x) are horizontal, 0 (N, -y) and 2 (S, +y)
+    // vertical: (tx, ty) is on the ray iff its offset across the ray is 0 and
+    // its distance along it is 1..L.  Selects, not integer multiplies, and
+    // bitwise conditions (no divergent branches).
     const int rx = tx - x, ry = ty - y;
-    const int j = rx * dx + ry * dy;
-    // bitwise (not short-circuit) conditions: no divergent branches
-    return ((rx == j * dx) & (ry == j * dy) & (j >= 1) & (j <= L)) ? j : 0;
+    const bool horiz = ad & 1;
+    const int along = horiz ? rx : ry, across = horiz ? ry : rx;
+    const int j = (ad == 1 || ad == 2) ? along : -along;
+    return ((across == 0) & (j >= 1) & (j <= L)) ? j : 0;
 }
 
 // Geometry of one relative direction d of an observation, packed in a word:
