@@ -253,7 +253,7 @@ enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3 };
 
 template <int NT, int EM>
 __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int M, int N, int col0, const Epi& ep,
-                                             int lane) {
+                                             const float* sbias, int lane) {
     const int rq = 4 * (lane >> 4);  // first of this lane's four rows (within the tile)
     uint32_t bits[kMaskWords] = {0u, 0u, 0u};
     if (EM == EM_BWD) {
@@ -264,7 +264,9 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
 #pragma unroll
     for (int c = 0; c < NT; c++) {
         const int col = col0 + 16 * c + (lane & 15);
-        const float bv = (EM != EM_BWD && ep.bias && col < N) ? ep.bias[col] : 0.f;
+        // the unit's bias sits in LDS: a global load here would make every column
+        // wait (vmcnt) for the previous columns' stores
+        const float bv = (EM != EM_BWD && ep.bias) ? sbias[16 * c + (lane & 15)] : 0.f;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const int row = 16 * rt + rq + g, bit = 4 * c + g;
@@ -365,6 +367,7 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
     // one stage run while the DMA into the other is in flight
     __shared__ __attribute__((aligned(16))) uint16_t sB0[C::kLen0];
     __shared__ __attribute__((aligned(16))) uint16_t sB1[C::kStageB];
+    __shared__ float sbias[16 * NT];  // the unit's bias columns (EM_F32 / EM_FWD)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // workgroup g takes units g, g + G, ...  XCD-aware unit order: units u and
@@ -379,6 +382,10 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         AS as;
         as.init(A, rt, nks, M, lda, K);
         const uint16_t* Bg = B + (size_t)cb * NT * nks * kBlk;
+        if (EM != EM_BWD && EM != EM_TP && ep.bias && threadIdx.x < 16 * NT) {  // visible after the prologue barrier
+            const int col = cb * 16 * NT + threadIdx.x;
+            sbias[threadIdx.x] = col < N ? ep.bias[col] : 0.f;
+        }
 
         f32x4 acc[NT];
 #pragma unroll
@@ -401,7 +408,7 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         if (EM == EM_TP)
             epilogue_tp<NT>(acc, reinterpret_cast<float*>(sB0) + wave * 16 * 36, rt, M, N, ep, lane);
         else
-            epilogue_f32<NT, EM>(acc, rt, M, N, cb * 16 * NT, ep, lane);
+            epilogue_f32<NT, EM>(acc, rt, M, N, cb * 16 * NT, ep, sbias, lane);
         // the next unit's DMA overwrites the epilogue slices: LDS reads done everywhere
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
