@@ -255,6 +255,7 @@ template <int NT, int EM>
 __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int M, int N, int col0, const Epi& ep,
                                              const float* sbias, int lane) {
     const int rq = 4 * (lane >> 4);  // first of this lane's four rows (within the tile)
+    const float* sb = sbias + (lane & 15);  // one base register, column c at immediate offset 64 c
     uint32_t bits[kMaskWords] = {0u, 0u, 0u};
     if (EM == EM_BWD) {
         const uint32_t* mb = ep.mbits_in + ((size_t)rt * 64 + lane) * kMaskWords;
@@ -266,7 +267,7 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
         const int col = col0 + 16 * c + (lane & 15);
         // the unit's bias sits in LDS: a global load here would make every column
         // wait (vmcnt) for the previous columns' stores
-        const float bv = (EM != EM_BWD && ep.bias) ? sbias[16 * c + (lane & 15)] : 0.f;
+        const float bv = (EM != EM_BWD && ep.bias) ? sb[16 * c] : 0.f;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const int row = 16 * rt + rq + g, bit = 4 * c + g;
@@ -365,9 +366,9 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
     using C = Cfg<NT>;
     // two distinct LDS objects: the compiler's alias scopes then let a B read of
     // one stage run while the DMA into the other is in flight
+    __shared__ float sbias[16 * NT];  // the unit's bias columns (EM_F32 / EM_FWD); first: small LDS offsets
     __shared__ __attribute__((aligned(16))) uint16_t sB0[C::kLen0];
     __shared__ __attribute__((aligned(16))) uint16_t sB1[C::kStageB];
-    __shared__ float sbias[16 * NT];  // the unit's bias columns (EM_F32 / EM_FWD)
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // workgroup g takes units g, g + G, ...  XCD-aware unit order: units u and
