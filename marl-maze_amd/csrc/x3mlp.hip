@@ -384,8 +384,10 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         as.init(A, rt, nks, M, lda, K);
         const uint16_t* Bg = B + (size_t)cb * NT * nks * kBlk;
         if (EM != EM_BWD && EM != EM_TP && ep.bias && threadIdx.x < 16 * NT) {  // visible after the prologue barrier
-            const int col = cb * 16 * NT + threadIdx.x;
-            sbias[threadIdx.x] = col < N ? ep.bias[col] : 0.f;
+            int t = threadIdx.x;
+            asm volatile("" : "+v"(t));  // recomputed per unit, not a loop-invariant address held (spilled) across it
+            const int col = cb * 16 * NT + t;
+            sbias[t] = col < N ? ep.bias[col] : 0.f;
         }
 
         f32x4 acc[NT];
