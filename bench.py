@@ -82,9 +82,9 @@ def main():
 
     # MARLMAZE_DP_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
     # the default is nccl (= RCCL) with one rank per GPU
-    dp = DP.from_env(backend=os.environ.get("MARLMAZE_DP_BACKEND"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))  # bind the GPU before the process group
+    dp = DP.from_env(backend=os.environ.get("MARLMAZE_DP_BACKEND"))  # (from_env binds it too, and passes device_id)
     world = dp.world
     if world != a.gpus and dp.rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)

@@ -86,11 +86,16 @@ class PPO:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
-        if tuned_gemms and self.device.type == "cuda":  # pre-tuned library GEMM choice (gemm_tuning.py)
+        if tuned_gemms and self.device.type == "cuda":
+            # pre-tuned library GEMM choice (gemm_tuning.py).  Process-wide side effect: TunableOp is
+            # switched on (lookup only, no tuning) for every later torch GEMM of this process, which
+            # then picks the recorded solution for shapes in the file; tuned_gemms=False leaves it off
             enable_tuned_gemms()
-        # networks are built on the CPU right after the seed, like PPO.py:7,16-17
+        # networks are built on the CPU right after the seed, like PPO.py:7,16-17; only the CPU
+        # generator is seeded (torch.manual_seed would also reset the caller's CUDA streams) and
+        # its state is restored afterwards
         g = torch.random.get_rng_state()
-        torch.manual_seed(seed)
+        torch.default_generator.manual_seed(seed)
         self.actor = Actor([264, 264, 264], parity_mode=parity_mode).to(self.device)
         self.critic = Critic(agent_amount, hidden_sizes=[64, 64]).to(self.device)
         torch.random.set_rng_state(g)
@@ -117,6 +122,7 @@ class PPO:
         self.bootstrap = bootstrap
         self.sample_seed = (sample_seed if sample_seed is not None else random.getrandbits(63)) + 7919 * self.dp.rank
         self._sample_offset = 0
+        self._shuffle_gen = None
         self.model_path = model_path
         self.verbose = verbose and self.dp.rank == 0
         self.save = save
@@ -239,7 +245,10 @@ class PPO:
         lp = (lp + torch.log(p)).view(M, 2)
         return lp[:, 0] + lp[:, 1]
 
-    def minibatch_step(self, obs, act, old_logp, adv, rtg, masks):
+    def minibatch_grads(self, obs, act, old_logp, adv, rtg, masks):
+        """Losses of PPO.py:62-80 and their gradients in every parameter's .grad
+        (before the all-reduce, the clipping and Adam).  Returns (actor_loss,
+        critic_loss) as 0-dim tensors."""
         V = self.critic(obs).view(-1)
         M = obs.shape[0]
         if obs.is_cuda:  # PPO.py:62-72 as two kernels (mm_ppo_loss / _bwd) on the [2M, 6] head logits
@@ -256,13 +265,19 @@ class PPO:
         self.actor_optim.zero_grad(set_to_none=True)  # backward assigns fresh gradients: no fill + add launches
         self.critic_optim.zero_grad(set_to_none=True)
         (actor_loss + critic_loss).backward()  # disjoint parameters: same grads as two backwards
+        return actor_loss.detach(), critic_loss.detach()
+
+    def minibatch_step(self, obs, act, old_logp, adv, rtg, masks):
+        """One iteration of PPO.py:58-85: losses, gradients, all-reduce (DP),
+        clip_grad_norm_ per network, Adam.  Returns (aloss, closs, gnorm_a, gnorm_c)."""
+        actor_loss, critic_loss = self.minibatch_grads(obs, act, old_logp, adv, rtg, masks)
         params = list(self.actor.parameters()) + list(self.critic.parameters())
         self.dp.allreduce_grads(params)
         gna = torch.nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad)
         gnc = torch.nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad)
         self.actor_optim.step()
         self.critic_optim.step()
-        return actor_loss.detach(), critic_loss.detach(), gna.detach(), gnc.detach()
+        return actor_loss, critic_loss, gna.detach(), gnc.detach()
 
     def update(self, b_obs, b_act, b_logp, b_masks, b_advs, b_vals, index_list=None, generator=None):
         """Update body of PPO.train; returns per-minibatch (aloss, closs, gnorm_a, gnorm_c) [K, 4]."""
@@ -271,11 +286,20 @@ class PPO:
         b_advs = (b_advs - mean) / (std + 1e-10)
         B = b_obs.shape[0]
         if index_list is None:
+            if generator is None:  # a per-rank stream (sample_seed differs by rank), not the global RNG
+                if self._shuffle_gen is None or self._shuffle_gen.device != b_obs.device:
+                    self._shuffle_gen = torch.Generator(device=b_obs.device)
+                    self._shuffle_gen.manual_seed(self.sample_seed ^ 0x5EED)
+                generator = self._shuffle_gen
             index_list = torch.randperm(B, device=b_obs.device, generator=generator)
         else:
             index_list = torch.as_tensor(index_list, device=b_obs.device, dtype=torch.long)
-        local_bs = min(self.batch_size // self.dp.world, B) if self.dp.active else self.batch_size
-        mb = local_bs // 5 if self.dp.active else self.mbatch_size
+        # the reference's minibatch loop spans batch_size (Q8); a batch smaller than that (explicit
+        # horizon * n_envs < batch_size) is used whole instead of yielding empty minibatches
+        local_bs = min(self.batch_size // self.dp.world, B)
+        mb = local_bs // 5 if (self.dp.active or local_bs < self.batch_size) else self.mbatch_size
+        if mb < 1:
+            raise ValueError(f"batch of {B} samples per rank is too small for 5 minibatches")
         # the reference shuffles once per batch (PPO.py:48-49): gather the batch into that order once,
         # so every minibatch is a contiguous slice (same rows, no per-minibatch gathers)
         used = min(B, ((local_bs + mb - 1) // mb) * mb)
@@ -302,8 +326,8 @@ class PPO:
         for epoch in range(self.epochs):
             b_obs, b_act, b_lp, b_sp, ep_lens, b_masks, b_advs, b_vals = self.get_batch()
             hist = self.update(b_obs, b_act, b_lp, b_masks, b_advs, b_vals)
-            stats = dict(epoch=epoch, episodes=len(ep_lens), mean_len=float(np.mean(ep_lens)) if ep_lens else 0.0,
-                         mean_shortest=float(np.mean(b_sp)) if b_sp else 0.0,
+            episodes, mean_len, mean_short = self.dp.episode_stats(ep_lens, b_sp)  # all ranks' episodes
+            stats = dict(epoch=epoch, episodes=episodes, mean_len=mean_len, mean_shortest=mean_short,
                          actor_loss=float(hist[-1, 0]), critic_loss=float(hist[-1, 1]))
             self.history.append(stats)
             if self.verbose:  # PPO.py:37-44, condensed
@@ -383,13 +407,28 @@ class PPO:
                         "actor_optim": self.actor_optim.state_dict(),
                         "critic_optim": self.critic_optim.state_dict()}), self.model_path)
 
+    def load_optim_state(self, opt, state):
+        """Adam.load_state_dict, keeping this build's Adam flavour: a state dict
+        written by the reference (CPU, fused=False) would otherwise switch the
+        GPU optimizer to the unfused path (the saved hyper-parameters replace the
+        group's).  The fused kernel keeps ``step`` as an fp32 device tensor."""
+        opt.load_state_dict(state)
+        fused = self.device.type == "cuda"
+        for group in opt.param_groups:
+            group["fused"] = fused or None
+            group["foreach"] = None
+            for p in group["params"]:
+                st = opt.state.get(p)
+                if st and "step" in st and fused:
+                    st["step"] = torch.as_tensor(st["step"], dtype=torch.float32, device=p.device).reshape(())
+
     def load_parameters(self):
         if os.path.exists(self.model_path):
             sd = torch.load(self.model_path, weights_only=True, map_location=self.device)
             self.actor.load_state_dict(sd["actor"])
             self.critic.load_state_dict(sd["critic"])
-            self.actor_optim.load_state_dict(sd["actor_optim"])
-            self.critic_optim.load_state_dict(sd["critic_optim"])
+            self.load_optim_state(self.actor_optim, sd["actor_optim"])
+            self.load_optim_state(self.critic_optim, sd["critic_optim"])
             if self.verbose:
                 print("successfuly loaded existing parameters")
             return True

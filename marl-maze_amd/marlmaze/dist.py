@@ -9,7 +9,8 @@ independent, so rollout and GAE need no communication; the exchange steps are
 2. one all-reduce of a single flat fp32 bucket holding every actor AND critic
    gradient per minibatch step (278,383 params = 1.11 MB), averaged, before
    clip_grad_norm_ so the clipped global norm is identical on every rank;
-3. per-epoch statistics.
+3. per-epoch statistics (episodes finished, their lengths and shortest
+   paths: three fp64 sums, ``episode_stats``).
 
 Backend "nccl" is RCCL on ROCm (xGMI inside the node); "gloo" for CPU tests.
 """
@@ -34,14 +35,26 @@ class DP:
 
     @staticmethod
     def from_env(backend=None):
-        """torchrun-style env (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT)."""
+        """torchrun-style env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR /
+        MASTER_PORT).  Binds the process to GPU ``LOCAL_RANK`` (modulo the
+        visible devices, so a gloo rehearsal may put several ranks on one GPU)
+        BEFORE the process group exists, and hands that device to RCCL, so the
+        communicator, ``PPO``'s default device and every barrier agree."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         if world <= 1:
             return DP.single()
+        local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+        dev = None
+        if torch.cuda.is_available():
+            dev = torch.device("cuda", local % torch.cuda.device_count())
+            torch.cuda.set_device(dev)
         if not dist.is_initialized():
             if backend is None:
-                backend = "nccl" if torch.cuda.is_available() else "gloo"
-            dist.init_process_group(backend=backend)
+                backend = "nccl" if dev is not None else "gloo"
+            if backend == "nccl":
+                dist.init_process_group(backend=backend, device_id=dev)
+            else:
+                dist.init_process_group(backend=backend)
         return DP(dist.get_rank(), dist.get_world_size())
 
     @property
@@ -86,6 +99,18 @@ class DP:
         mean = tot / n
         var = (sq - n * mean * mean) / (n - 1)
         return mean.to(x.dtype), var.clamp_min(0).sqrt().to(x.dtype)
+
+    def episode_stats(self, ep_lens, shortest):
+        """(episodes, mean exit time, mean shortest path) over every rank's
+        finished episodes (the figures PPO.py:37-44 prints)."""
+        s = torch.tensor([float(len(ep_lens)), float(sum(ep_lens)), float(sum(shortest))], dtype=torch.float64)
+        if self.active:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+            s = s.to(dev)
+            dist.all_reduce(s, op=dist.ReduceOp.SUM)
+            s = s.cpu()
+        n = int(s[0])
+        return n, (float(s[1]) / n if n else 0.0), (float(s[2]) / n if n else 0.0)
 
     def allreduce_sum(self, t):
         if self.active:

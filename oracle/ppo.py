@@ -103,7 +103,7 @@ class OActor(nn.Module):
             self.mark_head.weight *= 0.01
 
     def forward(self, x):  # networks.py:31-41
-        x = torch.as_tensor(x, dtype=torch.float32).reshape(-1, OBS)
+        x = torch.as_tensor(x, dtype=self.move_head.weight.dtype).reshape(-1, OBS)
         x = self.attention(self.projection(x))
         for lin in self.layers:
             x = torch.relu(lin(x))
@@ -120,7 +120,7 @@ class OCritic(nn.Module):
             nn.init.orthogonal_(lin.weight)
 
     def forward(self, x):  # networks.py:96-102
-        x = torch.as_tensor(x, dtype=torch.float32).reshape(-1, self.agent_amount * OBS)
+        x = torch.as_tensor(x, dtype=self.layers[0].weight.dtype).reshape(-1, self.agent_amount * OBS)
         for lin in self.layers[:-1]:
             x = torch.relu(lin(x))
         return self.layers[-1](x)
@@ -147,6 +147,25 @@ def log_probs(actor, i, obs, act, masks):
     return lp_move + torch.log(p)
 
 
+def minibatch_grads(actor, critic, obs, act, old_lp, adv, rtg, masks, clip=0.2):
+    """The two losses of PPO.py:62-80 and their gradients (before clip_grad_norm_
+    and Adam).  Returns (actor_loss, critic_loss, {name: actor grad},
+    {name: critic grad}); works for fp32 or fp64 modules (inputs are cast)."""
+    dt = next(actor.parameters()).dtype
+    obs, adv, rtg, old_lp = (t.to(dt) for t in (obs, adv, rtg, old_lp))
+    V = critic(obs).squeeze()
+    cur = 0
+    for i in range(2):
+        cur = cur + log_probs(actor, i, obs, act, masks)
+    ratio = torch.exp(cur - old_lp)
+    aloss = -torch.mean(torch.min(ratio * adv, torch.clamp(ratio, 1 - clip, 1 + clip) * adv))
+    closs = torch.nn.MSELoss()(V, rtg)
+    ga = torch.autograd.grad(aloss, list(actor.parameters()))
+    gc = torch.autograd.grad(closs, list(critic.parameters()))
+    return (float(aloss.detach()), float(closs.detach()), {k: g for (k, _), g in zip(actor.named_parameters(), ga)},
+            {k: g for (k, _), g in zip(critic.named_parameters(), gc)})
+
+
 def minibatch_step(actor, critic, aopt, copt, obs, act, old_lp, adv, rtg, masks,
                    clip=0.2, max_grad=0.5):
     """One iteration of PPO.py:58-85.  Returns (actor_loss, critic_loss, gn_a, gn_c)."""
@@ -167,7 +186,7 @@ def minibatch_step(actor, critic, aopt, copt, obs, act, old_lp, adv, rtg, masks,
     closs.backward()
     gnc = torch.nn.utils.clip_grad_norm_(critic.parameters(), max_grad)
     copt.step()
-    return float(aloss), float(closs), float(gna), float(gnc)
+    return float(aloss.detach()), float(closs.detach()), float(gna), float(gnc)
 
 
 def update_epoch(actor, critic, aopt, copt, b_obs, b_act, b_lp, b_masks, b_advs, b_vals,

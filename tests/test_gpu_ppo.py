@@ -4,8 +4,7 @@ teacher-forced reference train() epoch, and the vectorised rollout loop.
 Tolerance: 1e-5 relative on losses / returns / logits (BASELINE parity bar),
 with a small absolute floor (1e-6) for values that are ~0 (the actor loss of a
 normalised advantage batch).  Parameters after Adam are compared at the scale
-of one Adam step (lr): Adam's first moments make an update lr*g/|g|, so a
-gradient that is ~0 on both sides may move a parameter by +-lr on one of them.
+of one Adam step in test_gpu_update_parity.py (with per-parameter gradients).
 """
 import numpy as np
 import pytest
@@ -78,12 +77,15 @@ def test_minibatch_update_matches_reference(golden):
                                                            t["rtgs"], t["masks"]))
     for got, ref in ((al, n["actor_loss"]), (cl, n["critic_loss"]), (ga, n["actor_gnorm"]), (gc, n["critic_gnorm"])):
         assert abs(got - float(ref)) <= RTOL * abs(float(ref)) + ATOL, (got, float(ref))
-    for k, p in ag.actor.state_dict().items():
-        np.testing.assert_allclose(p.cpu().numpy(), n["actor_after/" + k], rtol=0, atol=2.1 * 0.00014)
+    # parameters after the step: test_gpu_update_parity.py (per-tensor Delta p vs actor_after / critic_after)
 
 
 def test_train_epoch_teacher_forced(golden):
-    """The reference's recorded PPO.train() epoch (batch 600) replayed on the GPU."""
+    """The reference's recorded PPO.train() epoch (batch 600) replayed on the GPU,
+    free-running: parameters drift from the reference's by summation-order
+    rounding amplified through 25 Adam steps, so minibatches after the first are
+    held to 1e-4 here; test_gpu_update_parity.py teacher-forces the oracle's
+    parameters and Adam state before every minibatch and holds all 25 to 1e-5."""
     t = golden("train_small")
     n = golden("nets")
     ag = _agent(n_envs=64, batch_size=600, lr=0.00014)
