@@ -35,35 +35,57 @@ from marlmaze.dist import DP  # noqa: E402
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def cpu_baseline(seconds=12.0, size=10, max_t=1200):
-    """The oracle's single-maze PPO.train() port on the host cores (bounded sample)."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4):
+    """One reference PPO.train() epoch (PPO.py:33-87) of the oracle's port: a
+    single 10x10 maze, batch_size 15000 (whole episodes until more than that
+    are stored, PPO.py:108-141), then 5 x 5 minibatch updates of 3,000."""
     from oracle.env import OracleEnv
     from oracle.ppo import CpuPPOPort
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     env = OracleEnv(1, default_size=(size, size), max_timestep=max_t, seeds=[0])
-    port = CpuPPOPort(env, batch_size=15000, lr=1.4e-4)
-    # rollout: as many steps as fit in ~2/3 of the budget (PPO.py:108-141 per step)
+    port = CpuPPOPort(env, batch_size=batch_size, lr=lr)
     t0 = time.time()
-    steps = 0
-    chunk = 200
-    batches = []
-    while time.time() - t0 < seconds * 0.66:
-        n, batch = port.get_batch(max_steps=chunk)
-        steps += n
-        batches.append(batch)
+    steps, batch = port.get_batch()
     t_roll = time.time() - t0
-    merged = [torch.cat([b[k] for b in batches]) for k in range(6)]
-    port.batch_size = len(merged[0]) - len(merged[0]) % 5
     t1 = time.time()
-    hist = port.update(merged)  # 5 x 5 minibatch updates of batch_size//5 (PPO.py:51-85)
+    hist = port.update(batch)
     t_upd = time.time() - t1
-    return dict(value=steps / (t_roll + t_upd), unit="env-steps/s", cores=threads, kind="port",
-                sample=f"oracle CpuPPOPort (C env + torch CPU fp32, 1 maze {size}x{size}, max_t {max_t}): "
-                       f"{steps} rollout steps in {t_roll:.1f}s + {len(hist)} minibatch updates of "
-                       f"{port.batch_size // 5} in {t_upd:.1f}s",
-                rollout_env_steps_per_s=steps / t_roll, ppo_updates_per_s=len(hist) / t_upd)
+    return dict(threads=threads, env_steps=steps, epoch_s=t_roll + t_upd, rollout_s=t_roll, update_s=t_upd,
+                env_steps_per_s=steps / (t_roll + t_upd), rollout_env_steps_per_s=steps / t_roll,
+                ppo_updates_per_s=len(hist) / t_upd, minibatch=batch_size // 5, minibatches=len(hist))
+
+
+def cpu_baseline():
+    """BASELINE.md's CPU plan: one full train() epoch of
+    the CPU port at the box's CPU share of threads and at 1 thread.  The port's
+    environment is the C oracle (bit-exact to the reference's Python env, ~5x
+    faster than it: SURVEY §6), its networks / sampling / update are torch-CPU
+    fp32 like the reference's, so the figure OVERSTATES the reference's own
+    train() speed."""
+    n_cpu = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, n_cpu)
+    runs = [_cpu_epoch(share), _cpu_epoch(1)]
+    best = max(runs, key=lambda r: r["env_steps_per_s"])  # the faster setting (1 thread usually: tiny per-step ops)
+    return dict(value=best["env_steps_per_s"], unit="env-steps/s", cores=best["threads"], kind="port",
+                sample=f"one full PPO.train() epoch (batch_size 15000, lr 1.4e-4, 1 maze 10x10, max_timestep 1200) "
+                       f"of oracle.ppo.CpuPPOPort: C-oracle env (bit-exact, ~5x faster than the reference's Python "
+                       f"env) + torch-CPU fp32 actor/critic/Adam; {best['env_steps']} env-steps + "
+                       f"{best['minibatches']} minibatch updates of {best['minibatch']} in {best['epoch_s']:.1f} s "
+                       f"at {best['threads']} thread(s) (the faster of {share} and 1)",
+                os_cpu_count=n_cpu, cpu_model=_cpu_model(), threads_used=[r["threads"] for r in runs],
+                runs=runs)
 
 
 def main():
@@ -77,7 +99,6 @@ def main():
     ap.add_argument("--max-t", type=int, default=1200, help="max_timestep (main.py:20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM heuristics (gemm_tuning.py)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     a = ap.parse_args()
 
     # MARLMAZE_DP_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
@@ -178,7 +199,7 @@ def main():
     del n_updates
     if dp.rank == 0:
         if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
     if dp.active:
         dist.destroy_process_group()

@@ -105,6 +105,19 @@ typedef struct {
     mm_maze_t* mazes;              /* [n] */
     uint32_t* rng;                 /* [n, MM_RNG_WORDS] */
     int32_t* work;                 /* [n + 64] scratch (done list) */
+    /* Optional pre-generation (all four NULL: every reset generates inline).
+     * Maze generation depends only on the maze's own MT19937 stream
+     * (maze.py:170-259), so each maze's NEXT maze can be generated ahead, off
+     * the step's critical path, by mm_env_pregen on a side stream; a reset
+     * then copies it in.  gen_state[i]: 0 = next_* hold the next maze,
+     * 1 = pending (mm_env_pregen will generate it), 2 = mm_env_pregen is
+     * generating it, 3 = a reset is generating inline.  rng always holds the
+     * state after the CURRENT maze's generation (the reference's observable
+     * random state), next_rng the state after the next one. */
+    uint8_t* next_layout;          /* [n, layout_stride], 16-byte aligned */
+    mm_maze_t* next_mazes;         /* [n]: generation fields of the next maze */
+    uint32_t* next_rng;            /* [n, MM_RNG_WORDS] */
+    int32_t* gen_state;            /* [n] */
 } mm_env_t;
 
 /* Library version (major*100 + minor). */
@@ -143,6 +156,14 @@ int mm_env_step_timed(const mm_env_t* env, const int8_t* actions, float* obs, ui
 /* Maze.reset() for the mazes queued by the previous mm_env_step(auto_reset=2)
  * (writes their obs/mask rows; clears the queue). */
 int mm_env_reset_done(const mm_env_t* env, float* obs, uint8_t* masks, void* stream);
+
+/* Generate the next maze of every maze whose gen_state is 1 (pending) into
+ * next_layout / next_mazes / next_rng (needs the pre-generation buffers).
+ * Safe to run on a second stream concurrently with steps and resets of the
+ * same env: mazes are claimed with atomics, and a reset that finds its maze's
+ * next maze still being generated waits for it.  Replaces nothing in the
+ * reference (its build_maze runs inside Maze.reset, maze.py:55-72). */
+int mm_env_pregen(const mm_env_t* env, void* stream);
 
 /* Time-major GAE over [T, N] (PPO.py:193-203, episodes concatenated in time,
  * done[t] = the transition at t ended its episode).  last_value [N] (may be

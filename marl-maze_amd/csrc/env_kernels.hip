@@ -98,6 +98,7 @@ __global__ void k_seed(mm_env_t env, const uint64_t* __restrict__ seeds) {
     mm_maze_t z = {};
     z.kx = z.ky = -1;
     env.mazes[m] = z;
+    if (env.gen_state) env.gen_state[m] = 1;  // a new stream: any pre-generated next maze is stale
 }
 
 // ---------------------------------------------------------------------------
@@ -110,6 +111,7 @@ struct GenLds {
     uint8_t pdir[kMaxCells];     // on-path cells: direction toward the end
     int16_t depth[kMaxCells];    // tree depth from start
     int16_t stack[kMaxCells];    // DFS stack (cell indices)
+    int claim;                   // pre-generation protocol: the state lane 0 found / claimed
 };
 
 // Maze.build_maze + set_start/end/key (maze.py:170-259), wave-uniform.
@@ -266,28 +268,32 @@ __device__ bool generate(const mm_env_t& env, GenLds& g, WaveRng& rng, int& w, i
     return kx >= 0;
 }
 
-__device__ void generate_one(const mm_env_t& env, GenLds& g, int m) {
+// One maze generation from the MT state rs_in (624 words + index) into the
+// layout row gl, the MT state after it into rs_out (may equal rs_in) and the
+// generation fields of hdr: for the current maze (next = false) the maze's
+// record is updated in place (t = 0, episode counters kept); for a
+// pre-generated next maze (next = true) hdr is written fresh.
+__device__ void generate_into(const mm_env_t& env, GenLds& g, const uint32_t* rs_in, uint32_t* rs_out, uint8_t* gl,
+                              mm_maze_t* hdr, bool next) {
     const int lane = threadIdx.x;
-    uint32_t* rs = env.rng + (size_t)m * MM_RNG_WORDS;
     {  // the 624 state words: all loads in flight before the LDS writes
         constexpr int kPer = (kMtN + 63) / 64;
         uint32_t t[kPer];
 #pragma unroll
-        for (int u = 0; u < kPer; u++) t[u] = lane + 64 * u < kMtN ? rs[lane + 64 * u] : 0u;
+        for (int u = 0; u < kPer; u++) t[u] = lane + 64 * u < kMtN ? rs_in[lane + 64 * u] : 0u;
 #pragma unroll
         for (int u = 0; u < kPer; u++)
             if (lane + 64 * u < kMtN) g.mt[lane + 64 * u] = t[u];
     }
     WaveRng rng;
     rng.mt = g.mt;
-    rng.idx = (int)rs[kMtN];
+    rng.idx = (int)rs_in[kMtN];
     rng.lane = lane;
     __syncthreads();
     int w, h, sx, sy, ex, ey, kx, ky, plen, p1x, p1y;
     const bool ok = generate(env, g, rng, w, h, sx, sy, ex, ey, kx, ky, plen, p1x, p1y);
     __syncthreads();
     // final layout bytes: cell | dir-to-exit << 2
-    uint8_t* gl = env.layout + (size_t)m * env.layout_stride;
     const int nc = w * h;
     for (int c = lane; c < nc; c += 64) {
         uint8_t b = g.cell[c];
@@ -298,11 +304,12 @@ __device__ void generate_one(const mm_env_t& env, GenLds& g, int m) {
         }
         gl[c] = b;
     }
-    for (int k = lane; k < kMtN; k += 64) rs[k] = g.mt[k];
-    if (lane == 0) rs[kMtN] = (uint32_t)rng.idx;
+    for (int k = lane; k < kMtN; k += 64) rs_out[k] = g.mt[k];
+    if (lane == 0) rs_out[kMtN] = (uint32_t)rng.idx;
     __syncthreads();
     if (lane == 0) {
-        mm_maze_t mz = env.mazes[m];
+        mm_maze_t mz = {};
+        if (!next) mz = *hdr;
         mz.t = 0;
         mz.w = (int8_t)w; mz.h = (int8_t)h;
         mz.ex = (int8_t)ex; mz.ey = (int8_t)ey;
@@ -311,7 +318,120 @@ __device__ void generate_one(const mm_env_t& env, GenLds& g, int m) {
         mz.path_len = (int16_t)plen;
         mz.spawn1 = p1x | (p1y << 8);  // second cell of the shortest path (agent 1's spawn)
         if (!ok) mz.status |= MM_ST_GEN_FAIL;
-        env.mazes[m] = mz;
+        *hdr = mz;
+    }
+}
+
+__device__ __forceinline__ void generate_one(const mm_env_t& env, GenLds& g, int m) {
+    uint32_t* rs = env.rng + (size_t)m * MM_RNG_WORDS;
+    generate_into(env, g, rs, rs, env.layout + (size_t)m * env.layout_stride, env.mazes + m, false);
+}
+
+// ---------------------------------------------------------------------------
+// pre-generation protocol (gen_state, see marlmaze.h)
+// ---------------------------------------------------------------------------
+enum { kGenReady = 0, kGenPending = 1, kGenRunning = 2, kGenInline = 3 };
+
+__device__ __forceinline__ int gs_load(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gs_store(int32_t* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool gs_cas(int32_t* p, int expect, int v) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Maze.reset()'s generation for maze m (one wavefront): the pre-generated
+// next maze copied in when it is ready, else generated inline (claimed so a
+// concurrent mm_env_pregen leaves it alone); a next maze still being
+// generated on the other stream is waited for.  Afterwards the maze's next
+// maze is pending again.
+__device__ void reset_one(const mm_env_t& env, GenLds& g, int m) {
+    if (!env.gen_state) {
+        generate_one(env, g, m);
+        return;
+    }
+    const int lane = threadIdx.x;
+    int32_t* st = env.gen_state + m;
+    if (lane == 0) {
+        int v;
+        while (true) {
+            v = gs_load(st);
+            if (v == kGenReady) break;
+            if (v == kGenPending && gs_cas(st, kGenPending, kGenInline)) {
+                v = kGenInline;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);  // kGenRunning: the pre-generation in flight finishes by itself
+        }
+        g.claim = v;
+    }
+    __syncthreads();
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // every lane reads what the pre-generation released
+    if (g.claim == kGenReady) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const int nv = env.layout_stride >> 4;  // layout_stride % 16 handled below
+        const u32x4* src = reinterpret_cast<const u32x4*>(env.next_layout + (size_t)m * env.layout_stride);
+        uint8_t* dst = env.layout + (size_t)m * env.layout_stride;
+        if ((env.layout_stride & 15) == 0) {
+            for (int k = lane; k < nv; k += 64) reinterpret_cast<u32x4*>(dst)[k] = src[k];
+        } else {
+            const uint8_t* sb = env.next_layout + (size_t)m * env.layout_stride;
+            for (int k = lane; k < env.layout_stride; k += 64) dst[k] = sb[k];
+        }
+        const uint32_t* rn = env.next_rng + (size_t)m * MM_RNG_WORDS;
+        uint32_t* rc = env.rng + (size_t)m * MM_RNG_WORDS;
+        for (int k = lane; k < MM_RNG_WORDS; k += 64) rc[k] = rn[k];
+        if (lane == 0) {
+            const mm_maze_t nx = env.next_mazes[m];
+            mm_maze_t mz = env.mazes[m];
+            mz.t = 0;
+            mz.w = nx.w; mz.h = nx.h;
+            mz.ex = nx.ex; mz.ey = nx.ey;
+            mz.kx = nx.kx; mz.ky = nx.ky;
+            mz.sx = nx.sx; mz.sy = nx.sy;
+            mz.path_len = nx.path_len;
+            mz.spawn1 = nx.spawn1;
+            mz.status |= nx.status;
+            env.mazes[m] = mz;
+        }
+    } else {
+        generate_one(env, g, m);
+    }
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // the new rng row before the pending flag
+    __syncthreads();
+    if (lane == 0) gs_store(st, kGenPending);
+}
+
+// mm_env_pregen: every pending maze's next maze, generated from its current
+// MT state.  A block (one wavefront) scans 64 mazes' states with one load per
+// lane, then generates the pending ones, each claimed with a CAS.  Usually
+// only a few mazes per step are pending, so the launch is mostly the scan.
+__global__ __launch_bounds__(64) void k_pregen(mm_env_t env) {
+    __shared__ GenLds g;
+    const int lane = threadIdx.x;
+    for (int base = blockIdx.x * 64; base < env.n; base += gridDim.x * 64) {
+        const int mine = base + lane;
+        const bool pend = mine < env.n && __hip_atomic_load(env.gen_state + mine, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT) == kGenPending;
+        uint64_t todo = __ballot(pend);
+        while (todo) {
+            const int m = base + __ffsll((unsigned long long)todo) - 1;
+            todo &= todo - 1;
+            if (lane == 0) g.claim = gs_cas(env.gen_state + m, kGenPending, kGenRunning);
+            __syncthreads();
+            if (g.claim) {
+                __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the rng row the reset released
+                generate_into(env, g, env.rng + (size_t)m * MM_RNG_WORDS, env.next_rng + (size_t)m * MM_RNG_WORDS,
+                              env.next_layout + (size_t)m * env.layout_stride, env.next_mazes + m, true);
+                __atomic_thread_fence(__ATOMIC_RELEASE);
+                __syncthreads();
+                if (lane == 0) gs_store(env.gen_state + m, kGenReady);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -366,7 +486,7 @@ __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __res
     for (int k = blockIdx.x; k < count; k += gridDim.x) {
         const int m = use_list ? env.work[kListOff + k] : k;
         if (!use_list && mask && !mask[m]) continue;
-        generate_one(env, g, m);
+        reset_one(env, g, m);
         __syncthreads();
     }
 }
@@ -641,6 +761,10 @@ inline int check_env(const mm_env_t* env) {
          reinterpret_cast<uintptr_t>(env->mazes)) & 15)
         return MM_E_ARG;
     if (env->difficulty < 1 || env->max_timestep < 1) return MM_E_ARG;
+    const int npg = !!env->next_layout + !!env->next_mazes + !!env->next_rng + !!env->gen_state;
+    if (npg != 0 && npg != 4) return MM_E_ARG;  // the pre-generation buffers come as a set
+    if ((reinterpret_cast<uintptr_t>(env->next_layout) | reinterpret_cast<uintptr_t>(env->next_mazes)) & 15)
+        return MM_E_ARG;
     return 0;
 }
 
@@ -668,7 +792,7 @@ extern "C" int mm_env_seed(const mm_env_t* env, const uint64_t* seeds, void* str
 
 static int launch_reset(const mm_env_t* env, const uint8_t* mask, int use_list, float* obs, uint8_t* masks,
                         hipStream_t s) {
-    int grid = use_list ? 2048 : (env->n < 16384 ? env->n : 16384);
+    int grid = use_list ? 512 : (env->n < 16384 ? env->n : 16384);
     hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), 0, s, *env, mask, use_list, obs, masks);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
@@ -713,6 +837,16 @@ extern "C" int mm_env_step_timed(const mm_env_t* env, const int8_t* actions, flo
 extern "C" int mm_env_step(const mm_env_t* env, const int8_t* actions, float* obs, uint8_t* masks, float* reward,
                            uint8_t* done, int32_t* ep_stats, int auto_reset, void* stream) {
     return mm_env_step_timed(env, actions, obs, masks, reward, done, ep_stats, auto_reset, stream, nullptr, nullptr);
+}
+
+extern "C" int mm_env_pregen(const mm_env_t* env, void* stream) {
+    int e = check_env(env);
+    if (e) return e;
+    if (!env->gen_state) return MM_E_ARG;
+    const int chunks = (env->n + 63) / 64;
+    const int grid = chunks < 256 ? chunks : 256;  // one block per CU: little LDS held beside the step kernels
+    hipLaunchKernelGGL(k_pregen, dim3(grid), dim3(64), 0, (hipStream_t)stream, *env);
+    return (int)hipGetLastError();
 }
 
 extern "C" int mm_env_reset_done(const mm_env_t* env, float* obs, uint8_t* masks, void* stream) {

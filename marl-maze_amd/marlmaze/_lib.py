@@ -32,7 +32,7 @@ AF_HAS_MARK = 64
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
-           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_gae", "mm_sample", "mm_head_sample",
+           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_sample", "mm_head_sample",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
@@ -50,6 +50,8 @@ class EnvDesc(ctypes.Structure):
         ("layout_stride", ctypes.c_int32),
         ("layout", ctypes.c_void_p), ("agents", ctypes.c_void_p), ("mazes", ctypes.c_void_p),
         ("rng", ctypes.c_void_p), ("work", ctypes.c_void_p),
+        ("next_layout", ctypes.c_void_p), ("next_mazes", ctypes.c_void_p), ("next_rng", ctypes.c_void_p),
+        ("gen_state", ctypes.c_void_p),
     ]
 
 
@@ -83,6 +85,8 @@ def lib():
         L.mm_env_step_timed.restype = i32
         L.mm_env_reset_done.argtypes = [ctypes.POINTER(EnvDesc), P, P, P]
         L.mm_env_reset_done.restype = i32
+        L.mm_env_pregen.argtypes = [ctypes.POINTER(EnvDesc), P]
+        L.mm_env_pregen.restype = i32
         L.mm_gae.argtypes = [P, P, P, P, i32, i32, f32, f32, P, P, P]
         L.mm_gae.restype = i32
         L.mm_sample.argtypes = [P, P, P, i32, u64, u64, P, P, P, P]

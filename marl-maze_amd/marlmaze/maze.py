@@ -66,7 +66,7 @@ class Maze:
             self._env = VecMaze(1, default_size=tuple(self.default_size), max_timestep=self.max_timestep,
                                 difficulty=self.difficulty, rand_start=self.rand_start, rand_sizes=self.rand_sizes,
                                 rand_range=tuple(self.rand_range), seeds=np.zeros(1, np.uint64),
-                                device=self._device)
+                                device=self._device, pregen=False)  # Python's global random feeds each reset
         return self._env
 
     def _sync(self, obs, masks):

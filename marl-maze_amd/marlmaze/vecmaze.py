@@ -46,7 +46,7 @@ class VecMaze:
 
     def __init__(self, n, default_size=(8, 8), max_timestep=3500, difficulty=1,
                  rand_start=False, rand_sizes=False, rand_range=(6, 12), seeds=None,
-                 seed_base=0, device=None):
+                 seed_base=0, device=None, pregen=True):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -75,18 +75,53 @@ class VecMaze:
         self.masks = torch.zeros((self.n, 2, _lib.MASK_DIM), dtype=torch.uint8, device=d)
         self.reward = torch.zeros(self.n, dtype=torch.float32, device=d)
         self.done = torch.zeros(self.n, dtype=torch.uint8, device=d)
+        # pre-generation (mm_env_pregen): each maze's next maze is generated ahead on a side stream,
+        # so a reset is a copy (the serial backtracker leaves the step's critical path)
+        self.pregen = bool(pregen)
+        if self.pregen:
+            self.next_layout = torch.ones((self.n, stride), dtype=torch.uint8, device=d)
+            self.next_mazes = torch.zeros((self.n, 32), dtype=torch.uint8, device=d)
+            self.next_rng = torch.zeros((self.n, _lib.RNG_WORDS), dtype=torch.int32, device=d)
+            self.gen_state = torch.ones(self.n, dtype=torch.int32, device=d)
+            self._gen_stream = torch.cuda.Stream(device=d)
+            # the side stream reads/writes these: the caching allocator must not hand their memory to
+            # another tensor before the side stream's queued work is done
+            for t in (self.rng, self.next_layout, self.next_mazes, self.next_rng, self.gen_state):
+                t.record_stream(self._gen_stream)
+            pg = (self.next_layout.data_ptr(), self.next_mazes.data_ptr(), self.next_rng.data_ptr(),
+                  self.gen_state.data_ptr())
+        else:
+            pg = (None, None, None, None)
         self._desc = _lib.EnvDesc(
             self.n, self.default_size[0], self.default_size[1], self.max_timestep, self.difficulty,
             int(self.rand_start), int(self.rand_sizes), self.rand_range[0], self.rand_range[1], stride,
             self.layout.data_ptr(), self.agents.data_ptr(), self.mazes.data_ptr(), self.rng.data_ptr(),
-            self.work.data_ptr())
+            self.work.data_ptr(), *pg)
         self.seed(seeds if seeds is not None else np.arange(self.n, dtype=np.uint64) + np.uint64(seed_base))
 
     # ------------------------------------------------------------------
     # hot path
     # ------------------------------------------------------------------
+    def _kick_pregen(self):
+        """Queue mm_env_pregen on the side stream, after everything queued so far
+        on the current stream (the resets that left mazes pending).  The current
+        stream never waits for it: a reset whose next maze is not ready yet
+        generates it itself, or waits for the one in flight (gen_state)."""
+        if not self.pregen:
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self._gen_stream.wait_stream(cur)
+        with torch.cuda.stream(self._gen_stream):
+            _lib.check(_lib.lib().mm_env_pregen(ctypes.byref(self._desc), _lib.stream_ptr()), "mm_env_pregen")
+
+    def _quiesce_pregen(self):
+        """The current stream waits for the side stream (before the MT rows are rewritten)."""
+        if self.pregen:
+            torch.cuda.current_stream(self.device).wait_stream(self._gen_stream)
+
     def seed(self, seeds):
         """random.seed(seeds[i]) for every maze; agents as Agent.__init__."""
+        self._quiesce_pregen()
         s = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64).reshape(self.n))
         st = torch.from_numpy(s.view(np.int64)).to(self.device)
         _lib.check(_lib.lib().mm_env_seed(ctypes.byref(self._desc), _lib.ptr(st), _lib.stream_ptr()),
@@ -102,6 +137,8 @@ class VecMaze:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
         _lib.check(_lib.lib().mm_env_reset(ctypes.byref(self._desc), _lib.ptr(m), _lib.ptr(obs),
                                            _lib.ptr(masks), _lib.stream_ptr()), "mm_env_reset")
+        self._reset_mask_keep = m  # read by the kernel after this call returns
+        self._kick_pregen()
         return obs, masks
 
     def step(self, actions, auto_reset=True, obs=None, masks=None, reward=None, done=None, ep_stats=None,
@@ -134,6 +171,8 @@ class VecMaze:
                                                     _lib.ptr(masks), _lib.ptr(reward), _lib.ptr(done),
                                                     _lib.ptr(ep_stats), int(auto_reset), _lib.stream_ptr(), e0, e1),
                        "mm_env_step_timed")
+        if int(auto_reset) == 1:
+            self._kick_pregen()
         return obs, masks, reward, done
 
     def reset_done(self, obs=None, masks=None):
@@ -142,6 +181,7 @@ class VecMaze:
         masks = self.masks if masks is None else masks
         _lib.check(_lib.lib().mm_env_reset_done(ctypes.byref(self._desc), _lib.ptr(obs), _lib.ptr(masks),
                                                 _lib.stream_ptr()), "mm_env_reset_done")
+        self._kick_pregen()
         return obs, masks
 
     # ------------------------------------------------------------------
@@ -172,8 +212,11 @@ class VecMaze:
         return self.rng[i].cpu().numpy().view(np.uint32).copy()
 
     def set_rng(self, i, state625):
+        self._quiesce_pregen()
         st = np.ascontiguousarray(np.asarray(state625, np.uint32)).view(np.int32)
         self.rng[i].copy_(torch.from_numpy(st))
+        if self.pregen:
+            self.gen_state[i] = 1  # the pre-generated next maze came from the old state
 
     def shortest_path(self, i):
         """Reconstruct Maze.shortest_path (start -> end) from the exit table."""

@@ -44,7 +44,20 @@ def test_library_exports_every_declared_symbol():
 def test_struct_mirrors_match_header():
     h = open(HEADER).read()
     assert "int32_t spawn1;" in h and AGENT_DTYPE.itemsize == 32 and MAZE_DTYPE.itemsize == 32
-    assert _lib.EnvDesc.layout.offset == 40 and ctypes_size(_lib.EnvDesc) == 80
+    # every field offset and the size of mm_env_t as the C compiler lays it out
+    import subprocess
+    import tempfile
+    fields = [f for f, _ in _lib.EnvDesc._fields_]
+    prog = ("#include <stddef.h>\n#include <stdio.h>\n#include \"marlmaze.h\"\nint main(void){printf(\"%zu\\n\", "
+            "sizeof(mm_env_t));" + "".join(f'printf("%zu\\n", offsetof(mm_env_t, {f}));' for f in fields) + "return 0;}")
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "m.c"), "w").write(prog)
+        subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", os.path.join(d, "m"), os.path.join(d, "m.c")],
+                       check=True)
+        out = [int(v) for v in subprocess.run([os.path.join(d, "m")], capture_output=True, text=True,
+                                              check=True).stdout.split()]
+    assert out[0] == ctypes_size(_lib.EnvDesc)
+    assert out[1:] == [getattr(_lib.EnvDesc, f).offset for f in fields]
     for name, val in (("MM_OBS_DIM", _lib.OBS_DIM), ("MM_MASK_DIM", _lib.MASK_DIM),
                       ("MM_RNG_WORDS", _lib.RNG_WORDS), ("MM_MAX_SIDE", _lib.MAX_SIDE)):
         assert re.search(rf"#define {name} {val}\b", h), name

@@ -209,3 +209,41 @@ def test_reset_mask_and_independence():
         single.reset()
         assert np.array_equal(single.layouts()[0], lay1[j])
         assert np.array_equal(single.get_rng(0), big.get_rng(j))
+
+
+@pytest.mark.parametrize("cfg", [dict(default_size=(10, 10), max_timestep=3),
+                                 dict(default_size=(2, 2), max_timestep=1),
+                                 dict(default_size=(20, 20), max_timestep=5)])
+def test_pregeneration_is_invisible(cfg):
+    """mm_env_pregen (next mazes generated ahead on a side stream, resets copy
+    them in) gives bit-identical layouts, MT states, observations and episode
+    records to inline generation -- also when many resets are queued with no
+    host synchronisation, so that resets find their next maze pending (and
+    generate it inline) or in flight (and wait for it)."""
+    n, steps = 4096, 40
+    seeds = np.arange(n, dtype=np.uint64) * np.uint64(31) + np.uint64(5)
+    envs = [VecMaze(n, seeds=seeds, pregen=p, **cfg) for p in (False, True)]
+    acts = torch.randint(0, 2, (steps, n, 2, 2), generator=torch.Generator().manual_seed(0)).to(torch.int8).cuda()
+    outs = []
+    for env in envs:
+        env.reset()
+        rec = []
+        for s in range(steps):  # stay (move 4) or 0..1 moves: legality does not matter for this comparison
+            a = acts[s].clone()
+            a[..., 0] = torch.where(a[..., 0] == 0, 4, 0).to(torch.int8)
+            if s % 2:
+                env.step(a, auto_reset=2)
+                env.reset_done()
+            else:
+                env.step(a, auto_reset=True)
+            rec.append(env.obs.clone())
+        torch.cuda.synchronize()
+        outs.append((torch.stack(rec).cpu(), env.layout.cpu(), env.rng.cpu(), env.mazes.cpu(), env.agents.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    torch.cuda.synchronize()
+    st = envs[1].gen_state.cpu()
+    assert ((st == 0) | (st == 1)).all()
+    envs[1]._kick_pregen()
+    torch.cuda.synchronize()
+    assert (envs[1].gen_state.cpu() == 0).all()  # every maze's next maze is ready after one idle pass

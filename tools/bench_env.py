@@ -22,10 +22,11 @@ ap.add_argument("--size", type=int, default=10)
 ap.add_argument("--steps", type=int, default=200)
 ap.add_argument("--warmup", type=int, default=50)
 ap.add_argument("--max-t", type=int, default=1200)
+ap.add_argument("--no-pregen", action="store_true", help="generate every reset inline (no side stream)")
 a = ap.parse_args()
 
 n = a.mazes
-env = VecMaze(n, default_size=(a.size, a.size), max_timestep=a.max_t)
+env = VecMaze(n, default_size=(a.size, a.size), max_timestep=a.max_t, pregen=not a.no_pregen)
 t0 = time.time()
 obs, masks = env.reset()
 torch.cuda.synchronize()
@@ -40,10 +41,10 @@ def one(i, ev=None):
     ops.sample(ml, kl, masks.view(2 * n, 6), seed=1, offset=i, actions=acts)
     if ev:
         ev[0].record(s)
-    env.step(acts.view(n, 2, 2), auto_reset=False, obs=obs, masks=masks)
+    env.step(acts.view(n, 2, 2), auto_reset=2, obs=obs, masks=masks)  # finished mazes queued (done list)
     if ev:
         ev[1].record(s)
-    env.reset(env.done, obs=obs, masks=masks)
+    env.reset_done(obs=obs, masks=masks)  # PPO.get_batch's reset (PPO.py:127-130); next mazes pre-generated
     if ev:
         ev[2].record(s)
 
