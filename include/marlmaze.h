@@ -176,6 +176,23 @@ int mm_env_pregen(const mm_env_t* env, void* stream);
 int mm_gae(const float* reward, const float* value, const uint8_t* done, const float* last_value, int T, int N,
            float gamma, float gamma_lambda, float* adv, float* rtg, void* stream);
 
+/* mm_gae with the algorithm chosen by the caller (mm_gae = MM_GAE_AUTO):
+ *   MM_GAE_COLUMN  one lane per column, reverse recursion (many columns);
+ *   MM_GAE_WALK    one lane per (column, chunk of t) running the episodes that
+ *                  end in its chunk (few columns, long T: the reference's
+ *                  whole-episode batches, PPO.py:108-141) -- bit-identical to
+ *                  MM_GAE_COLUMN, parallel across episodes;
+ *   MM_GAE_SCAN    one workgroup per column, affine-map suffix scan with
+ *                  wavefront shuffles -- parallel inside an episode,
+ *                  reassociated fp32 (not bit-exact; ~1e-7 relative);
+ *   MM_GAE_AUTO    COLUMN for N >= 16384 or short T, else WALK (bit-exact). */
+#define MM_GAE_AUTO 0
+#define MM_GAE_COLUMN 1
+#define MM_GAE_WALK 2
+#define MM_GAE_SCAN 3
+int mm_gae_ex(const float* reward, const float* value, const uint8_t* done, const float* last_value, int T, int N,
+              float gamma, float gamma_lambda, float* adv, float* rtg, int algo, void* stream);
+
 /* Sample one action per agent row (PPO.py:170-186): move ~ Categorical over
  * move_logits [M,5] masked to -inf where masks[:,0:5]==0; mark ~ Bernoulli(
  * sigmoid(mark_logit [M])) where masks[:,5] else 0.  Rows are (maze, agent)

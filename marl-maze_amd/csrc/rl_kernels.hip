@@ -8,6 +8,12 @@
 //               delta_t = (r_t + f32(g*V_{t+1}) * (1-d_{t+1})) - V_t
 //               A_t     = delta_t + f32(f32(g*lam) * A_{t+1})   (0 if d_t)
 //             (the d_{t+1} mask drops V_{L-1} from delta_{L-2}: quirk Q7).
+//   k_gae_walk  the same, bit-identical, for few columns and long T (whole-
+//             episode batches): parallel across episodes, one lane per
+//             (column, chunk) running the episodes that end in its chunk.
+//   k_gae_scan  the same recursion as an affine-map suffix scan (wavefront
+//             shuffles + LDS): parallel inside episodes, reassociated (fp32
+//             rounding differs; within 1e-5 relative).
 //   k_sample  PPO.get_action (PPO.py:170-186) for every agent row: masked
 //             categorical move + Bernoulli mark, per-agent and joint log-prob,
 //             counter-based Philox4x32-10 draws.
@@ -24,44 +30,172 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "marlmaze.h"
 
 namespace mm {
 
-__global__ void k_gae(const float* __restrict__ rew, const float* __restrict__ val, const uint8_t* __restrict__ done,
-                      const float* __restrict__ last_val, int T, int N, float g, float gl, float* __restrict__ adv,
-                      float* __restrict__ rtg) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    float a = 0.f;
-    // state carried from t+1: value and done flag
-    float v_next = last_val ? last_val[i] : 0.f;
-    bool have_next = last_val != nullptr;  // false: segment end == episode end
-    bool d_next = false;
-    for (int t = T - 1; t >= 0; t--) {
-        const size_t k = (size_t)t * N + i;
-        const float r = rew[k];
-        const float v = val[k];
-        // without a bootstrap value the segment end IS an episode end (done=1),
-        // so the reference's d_{t+1} mask also applies to delta_{T-2} (Q7)
-        const bool d = done[k] != 0 || (t == T - 1 && !last_val);
-        float delta;
-        if (d || !have_next) {
-            // the reference's `t+1 == len(ep)` branch: delta = r - V
-            delta = __fsub_rn(r, v);
-        } else {
-            float boot = __fmul_rn(g, v_next);
-            if (d_next) boot = __fmul_rn(boot, 0.f);
-            delta = __fsub_rn(__fadd_rn(r, boot), v);
-        }
-        const float scale = d ? 0.f : gl;
-        a = __fadd_rn(delta, __fmul_rn(scale, a));
-        adv[k] = a;
-        if (rtg) rtg[k] = __fadd_rn(a, v);  // b_rtgs = b_advs + b_vals (PPO.py:46)
-        v_next = v;
-        d_next = d;
+struct GaeArgs {
+    const float* rew;
+    const float* val;
+    const uint8_t* done;
+    const float* lv;  // last_value [N] or null
+    int T, N;
+    float g, gl;
+    float* adv;
+    float* rtg;  // or null
+};
+
+// delta_t of one position in the reference's operation order (header): `d` =
+// this transition ends the episode, `have_next` = a value exists at t+1 (the
+// next position or the bootstrap), `d_next` = the transition at t+1 ended its
+// episode (quirk Q7's mask)
+__device__ __forceinline__ float gae_delta(float r, float v, bool d, bool have_next, float v_next, bool d_next,
+                                           float g) {
+    if (d || !have_next) return __fsub_rn(r, v);  // the reference's `t+1 == len(ep)` branch
+    float boot = __fmul_rn(g, v_next);
+    if (d_next) boot = __fmul_rn(boot, 0.f);
+    return __fsub_rn(__fadd_rn(r, boot), v);
+}
+
+// without a bootstrap value the segment end IS an episode end (done = 1)
+__device__ __forceinline__ bool gae_end_at(const GaeArgs& a, int n, int t) {
+    return a.done[(size_t)t * a.N + n] != 0 || (t == a.T - 1 && !a.lv);
+}
+
+// Reverse sweep of column n over t = t_hi .. t_lo calling f(t, delta_t, d_t,
+// V_t) (f returns false to stop before position t).  The loads of kGaeU
+// positions are issued together: the sweep is latency-bound (one HBM round
+// trip per block instead of one per position).
+constexpr int kGaeU = 16;
+template <class F>
+__device__ __forceinline__ void gae_sweep(const GaeArgs& a, int n, int t_hi, int t_lo, F&& f) {
+    float v_next;
+    bool d_next, have_next;
+    if (t_hi + 1 < a.T) {
+        v_next = a.val[(size_t)(t_hi + 1) * a.N + n];
+        d_next = gae_end_at(a, n, t_hi + 1);
         have_next = true;
+    } else {
+        v_next = a.lv ? a.lv[n] : 0.f;
+        d_next = false;
+        have_next = a.lv != nullptr;
     }
+    for (int tb = t_hi; tb >= t_lo; tb -= kGaeU) {
+        float r[kGaeU], v[kGaeU];
+        uint8_t dd[kGaeU];
+#pragma unroll
+        for (int u = 0; u < kGaeU; u++) {
+            const int t = tb - u;
+            if (t >= t_lo) {
+                const size_t k = (size_t)t * a.N + n;
+                r[u] = a.rew[k];
+                v[u] = a.val[k];
+                dd[u] = a.done[k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kGaeU; u++) {
+            const int t = tb - u;
+            if (t < t_lo) break;
+            const bool d = dd[u] != 0 || (t == a.T - 1 && !a.lv);
+            const float delta = gae_delta(r[u], v[u], d, have_next, v_next, d_next, a.g);
+            if (!f(t, delta, d, v[u])) return;
+            v_next = v[u];
+            d_next = d;
+            have_next = true;
+        }
+    }
+}
+
+__device__ __forceinline__ void gae_store(const GaeArgs& a, int n, int t, float adv, float v) {
+    const size_t k = (size_t)t * a.N + n;
+    a.adv[k] = adv;
+    if (a.rtg) a.rtg[k] = __fadd_rn(adv, v);  // b_rtgs = b_advs + b_vals (PPO.py:46)
+}
+
+// one lane per maze column (many columns, short T): A_t = delta_t + f32(gl * A_{t+1}), 0-scaled at d_t
+__global__ void k_gae(GaeArgs a) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= a.N) return;
+    float acc = 0.f;
+    gae_sweep(a, n, a.T - 1, 0, [&](int t, float delta, bool d, float v) {
+        acc = __fadd_rn(delta, __fmul_rn(d ? 0.f : a.gl, acc));
+        gae_store(a, n, t, acc, v);
+        return true;
+    });
+}
+
+// Few columns, long T (the reference's whole-episode batches: T up to tens of
+// thousands): the column is cut into chunks of Lc positions, one lane per
+// (column, chunk), and each lane owns the episodes that END in its chunk.  It
+// runs each of them backward from its end to the position after the previous
+// episode's end -- the same serial recursion, in the same order, as k_gae, so
+// the result is bit-identical; the parallelism is across episodes (the
+// recursion restarts at every done, PPO.py:201).  The longest episode bounds
+// the time (<= max_timestep steps).
+__global__ void k_gae_walk(GaeArgs a, int Lc, int nch) {
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long)a.N * nch) return;
+    const int n = (int)(gid % a.N), j = (int)(gid / a.N);  // neighbouring lanes: neighbouring columns
+    const int t0 = j * Lc, t1 = min(a.T, t0 + Lc);
+    for (int e = t1 - 1; e >= t0; e--) {
+        if (!gae_end_at(a, n, e) && e != a.T - 1) continue;  // (T-1 with a bootstrap: the fragment's end)
+        float acc = 0.f;
+        gae_sweep(a, n, e, 0, [&](int t, float delta, bool d, float v) {
+            if (t < e && d) return false;  // the previous episode's end: this episode is done
+            acc = __fadd_rn(delta, __fmul_rn(d ? 0.f : a.gl, acc));
+            gae_store(a, n, t, acc, v);
+            return true;
+        });
+    }
+}
+
+// Long T, parallel INSIDE episodes (not bit-exact: the recursion is
+// reassociated).  A_t = delta_t + c_t A_{t+1} is an affine map of A_{t+1}, and
+// maps compose associatively, (P1, Q1) o (P2, Q2) = (P1 P2, P1 Q2 + Q1).  One
+// workgroup per column; thread i owns a contiguous chunk (thread order = time
+// order) and composes its chunk's map; a suffix scan of the maps with
+// wavefront shuffles (then across the 4 wavefronts through LDS) gives every
+// thread the advantage just after its chunk; a second sweep writes A_t.
+__global__ __launch_bounds__(256) void k_gae_scan(GaeArgs a) {
+    __shared__ float sP[4], sQ[4];
+    const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int per = (a.T + 255) / 256;
+    const int t0 = min(a.T, tid * per), t1 = min(a.T, t0 + per);
+    float P = 1.f, Q = 0.f;  // A(t0) = P A(t1) + Q
+    if (t1 > t0)
+        gae_sweep(a, n, t1 - 1, t0, [&](int, float delta, bool d, float) {
+            const float c = d ? 0.f : a.gl;
+            Q = __fadd_rn(delta, __fmul_rn(c, Q));
+            P = __fmul_rn(c, P);
+            return true;
+        });
+    // suffix scan inside the wavefront: lane l -> the map of lanes l .. 63
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float Pn = __shfl_down(P, off), Qn = __shfl_down(Q, off);
+        if (lane + off < 64) {
+            Q = __fadd_rn(__fmul_rn(P, Qn), Q);
+            P = __fmul_rn(P, Pn);
+        }
+    }
+    if (lane == 0) {
+        sP[w] = P;
+        sQ[w] = Q;
+    }
+    __syncthreads();
+    float carry = 0.f;  // A at the start of wavefront w + 1's chunks (A after the column's end = 0)
+    for (int ww = 3; ww > w; ww--) carry = __fadd_rn(__fmul_rn(sP[ww], carry), sQ[ww]);
+    const float P1 = __shfl_down(P, 1), Q1 = __shfl_down(Q, 1);
+    float acc = lane < 63 ? __fadd_rn(__fmul_rn(P1, carry), Q1) : carry;  // A(t1)
+    if (t1 > t0)
+        gae_sweep(a, n, t1 - 1, t0, [&](int t, float delta, bool d, float v) {
+            acc = __fadd_rn(delta, __fmul_rn(d ? 0.f : a.gl, acc));
+            gae_store(a, n, t, acc, v);
+            return true;
+        });
 }
 
 // ---------------------------------------------------------------------------
@@ -331,13 +465,33 @@ __global__ __launch_bounds__(256) void k_ppo_loss_bwd(const float* __restrict__ 
 
 using namespace mm;
 
+extern "C" int mm_gae_ex(const float* reward, const float* value, const uint8_t* done, const float* last_value,
+                         int T, int N, float gamma, float gamma_lambda, float* adv, float* rtg, int algo,
+                         void* stream) {
+    if (!reward || !value || !done || !adv || T < 0 || N < 0 || algo < MM_GAE_AUTO || algo > MM_GAE_SCAN)
+        return MM_E_ARG;
+    if (T == 0 || N == 0) return 0;
+    const GaeArgs a{reward, value, done, last_value, T, N, gamma, gamma_lambda, adv, rtg};
+    hipStream_t s = (hipStream_t)stream;
+    if (algo == MM_GAE_AUTO) algo = (N >= 16384 || T <= 2 * kGaeU) ? MM_GAE_COLUMN : MM_GAE_WALK;
+    if (algo == MM_GAE_COLUMN) {
+        hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, s, a);
+    } else if (algo == MM_GAE_WALK) {
+        // chunks of >= 16 positions, enough of them for ~16k lanes
+        const long want = (long)T * N / 16384;
+        const int Lc = (int)std::max<long>(16, std::min<long>(want, T));
+        const int nch = (T + Lc - 1) / Lc;
+        const long lanes = (long)N * nch;
+        hipLaunchKernelGGL(k_gae_walk, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, s, a, Lc, nch);
+    } else {
+        hipLaunchKernelGGL(k_gae_scan, dim3(N), dim3(256), 0, s, a);
+    }
+    return (int)hipGetLastError();
+}
+
 extern "C" int mm_gae(const float* reward, const float* value, const uint8_t* done, const float* last_value, int T,
                       int N, float gamma, float gamma_lambda, float* adv, float* rtg, void* stream) {
-    if (!reward || !value || !done || !adv || T < 0 || N < 0) return MM_E_ARG;
-    if (T == 0 || N == 0) return 0;
-    hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, reward, value, done,
-                       last_value, T, N, gamma, gamma_lambda, adv, rtg);
-    return (int)hipGetLastError();
+    return mm_gae_ex(reward, value, done, last_value, T, N, gamma, gamma_lambda, adv, rtg, MM_GAE_AUTO, stream);
 }
 
 extern "C" int mm_sample(const float* move_logits, const float* mark_logits, const uint8_t* masks, int M,

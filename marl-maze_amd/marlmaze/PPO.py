@@ -80,7 +80,8 @@ class PPO:
     def __init__(self, agent_amount, epochs=500, batch_size=15000, lr=0.0002, discount_rate=0.99, lam=0.95,
                  updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
                  seed=3234, sample_seed=None, device=None, model_path=MODEL_PATH, load=True, parity_mode=True,
-                 bootstrap=True, dp=None, verbose=True, save=True, tuned_gemms=True):
+                 bootstrap=True, dp=None, verbose=True, save=True, tuned_gemms=True, episode_batches=False,
+                 episode_chunk=64):
         self.maze = None  # wired by Maze.__init__ (maze.py:39-42), as in the reference
         self.dp = dp if dp is not None else DP.single()
         if device is None:
@@ -120,6 +121,9 @@ class PPO:
         self.horizon = int(horizon) if horizon else max(1, math.ceil(batch_size / (self.n_envs * self.dp.world)))
         self.env_config = env_config
         self.bootstrap = bootstrap
+        self.episode_batches = bool(episode_batches)  # the reference's whole-episode batches (_episode_batch)
+        self.episode_chunk = int(episode_chunk)
+        self._fresh = False  # the env was just reset (its first batch needs no reset of its own)
         self.sample_seed = (sample_seed if sample_seed is not None else random.getrandbits(63)) + 7919 * self.dp.rank
         self._sample_offset = 0
         self._shuffle_gen = None
@@ -169,6 +173,7 @@ class PPO:
             rtg=torch.zeros((T, n), dtype=torch.float32, device=d),
         )
         self.venv.reset(obs=self._bufs["obs"][0], masks=self._bufs["masks"][0])
+        self._fresh = True
 
     # ------------------------------------------------------------------
     # rollout (PPO.get_batch, PPO.py:89-152)
@@ -213,8 +218,98 @@ class PPO:
         b["obs"][0].copy_(b["obs"][self.horizon])
         b["masks"][0].copy_(b["masks"][self.horizon])
 
+    @torch.no_grad()
+    def _episode_batch(self):
+        """PPO.get_batch (PPO.py:89-152) over ``n_envs`` mazes, whole episodes only.
+
+        Every maze is reset (PPO.py:104) and all step together.  The batch ends
+        at the first step t* after which the steps of completed episodes (all
+        mazes) exceed ``batch_size`` (per rank under DP) -- with one maze that is
+        the reference's rule, the first episode end after more than
+        ``batch_size`` steps (PPO.py:126-141).  Episodes still running at t* are
+        dropped (the reference keeps only complete episodes).  Samples are
+        ordered maze by maze, each maze's episodes in time order (one maze: the
+        reference's order), and GAE runs on whole episodes (PPO.py:133; the
+        episode-parallel walk of mm_gae_ex, bit-exact).  No step runs past t*
+        (a maze finishing there would draw its next maze from its RNG stream,
+        which the reference never does): after step t at most n (t + 1) steps
+        can belong to completed episodes, so steps before t = batch_size // n
+        run in chunks of ``episode_chunk`` with one host synchronisation per
+        chunk, later ones one at a time.
+        """
+        self._ensure_env()
+        n, dev = self.n_envs, self.device
+        limit = self.batch_size // self.dp.world
+        if self._fresh:  # the state at the batch's first step
+            obs0, masks0 = self._bufs["obs"][0].clone(), self._bufs["masks"][0].clone()
+        else:
+            obs0 = torch.empty((n, 2, 65), dtype=torch.float32, device=dev)
+            masks0 = torch.empty((n, 2, 6), dtype=torch.uint8, device=dev)
+            self.venv.reset(obs=obs0, masks=masks0)  # PPO.py:104
+        self._fresh = False
+        head_w, head_b = self.actor.heads()
+        chunks = []
+        last_end = torch.full((n,), -1, dtype=torch.int64, device=dev)
+        t0, t_stop, end_at_stop = 0, None, None
+        t_min = limit // n  # the first step after which the batch can be full
+        while t_stop is None:
+            C = min(self.episode_chunk, t_min - t0) if t0 < t_min else 1
+            ch = dict(obs=torch.empty((C + 1, n, 2, 65), dtype=torch.float32, device=dev),
+                      masks=torch.empty((C + 1, n, 2, 6), dtype=torch.uint8, device=dev),
+                      act=torch.empty((C, n, 2, 2), dtype=torch.int8, device=dev),
+                      logp=torch.empty((C, n), dtype=torch.float32, device=dev),
+                      rowlogp=torch.empty((C, 2 * n), dtype=torch.float32, device=dev),
+                      val=torch.empty((C, n), dtype=torch.float32, device=dev),
+                      rew=torch.empty((C, n), dtype=torch.float32, device=dev),
+                      done=torch.empty((C, n), dtype=torch.uint8, device=dev),
+                      stats=torch.empty((C, n, 2), dtype=torch.int32, device=dev))
+            ch["obs"][0].copy_(obs0)
+            ch["masks"][0].copy_(masks0)
+            for t in range(C):
+                ch["val"][t] = self.critic(ch["obs"][t]).view(n)
+                h = self.actor.trunk(ch["obs"][t].view(2 * n, 65))
+                ops.head_sample(h, head_w, head_b, ch["masks"][t].view(2 * n, 6), self.sample_seed,
+                                self._sample_offset, actions=ch["act"][t].view(2 * n, 2), logp=ch["rowlogp"][t],
+                                joint_logp=ch["logp"][t])
+                self._sample_offset += 1
+                self.venv.step(ch["act"][t], auto_reset=True, obs=ch["obs"][t + 1], masks=ch["masks"][t + 1],
+                               reward=ch["rew"][t], done=ch["done"][t], ep_stats=ch["stats"][t])
+            chunks.append(ch)
+            obs0, masks0 = ch["obs"][C], ch["masks"][C]
+            # completed-episode steps after each step of the chunk: sum over mazes of (last end + 1)
+            tt = torch.arange(t0, t0 + C, device=dev).view(C, 1)
+            ends = torch.where(ch["done"].bool(), tt, torch.full_like(tt, -1))
+            ends = torch.maximum(torch.cummax(ends, 0).values, last_end.view(1, n))
+            filled = (ends + 1).sum(1)
+            hit = torch.nonzero(filled > limit)
+            if hit.numel():  # one host synchronisation per chunk; only the last chunk can hit (at its end)
+                k = int(hit[0, 0])
+                t_stop, end_at_stop = t0 + k, ends[k]
+            else:
+                last_end = ends[-1]
+                t0 += C
+        Ts = t_stop + 1  # == the steps taken (the last chunk ends at t_stop)
+        cat = {k: torch.cat([c[k][:c["act"].shape[0]] for c in chunks], 0)[:Ts]
+               for k in ("obs", "masks", "act", "logp", "val", "rew", "done", "stats")}
+        adv, rtg = ops.gae(cat["rew"], cat["val"], cat["done"], gamma=self.discount_rate, lam=self.lam)
+        keep = torch.arange(Ts, device=dev).view(Ts, 1) <= end_at_stop.view(1, n)
+        nt = torch.nonzero(keep.t())  # (maze, t), maze-major, t ascending
+        flat = nt[:, 1] * n + nt[:, 0]
+        B = flat.numel()
+        pick = lambda x, *shape: x.reshape(Ts * n, *shape)[flat]  # noqa: E731
+        st = pick(cat["stats"], 2)
+        fin = st[:, 0] > 0
+        out = (pick(cat["obs"], 2, 65), pick(cat["act"], 2, 2).float(), pick(cat["logp"]),
+               st[fin, 1].tolist(), st[fin, 0].tolist(), pick(cat["masks"], 2, 6).bool(), pick(adv), pick(cat["val"]))
+        self._episode_info = dict(t_stop=t_stop, samples=B, rtg=pick(rtg), act=cat["act"], done=cat["done"])
+        return out
+
     def get_batch(self):
-        """Reference 8-tuple (PPO.py:151-152), samples flattened time-major."""
+        """Reference 8-tuple (PPO.py:151-152).  Default: every maze advances
+        ``horizon`` steps, samples flattened time-major.  ``episode_batches``:
+        whole episodes only (_episode_batch)."""
+        if self.episode_batches:
+            return self._episode_batch()
         b = self.rollout()
         T, n = self.horizon, self.n_envs
         B = T * n

@@ -22,6 +22,8 @@ MAZES_PER_BLOCK = 32
 ST_GEN_FAIL = 1
 ST_BAD_MOVE = 2
 
+GAE_AUTO, GAE_COLUMN, GAE_WALK, GAE_SCAN = 0, 1, 2, 3  # mm_gae_ex algorithms
+
 AF_KNOWS_END = 1
 AF_SEES_END = 2
 AF_OTHER_KNOWS = 4
@@ -32,7 +34,7 @@ AF_HAS_MARK = 64
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
-           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_sample", "mm_head_sample",
+           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
@@ -89,6 +91,8 @@ def lib():
         L.mm_env_pregen.restype = i32
         L.mm_gae.argtypes = [P, P, P, P, i32, i32, f32, f32, P, P, P]
         L.mm_gae.restype = i32
+        L.mm_gae_ex.argtypes = [P, P, P, P, i32, i32, f32, f32, P, P, i32, P]
+        L.mm_gae_ex.restype = i32
         L.mm_sample.argtypes = [P, P, P, i32, u64, u64, P, P, P, P]
         L.mm_sample.restype = i32
         L.mm_head_sample.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P]

@@ -13,12 +13,17 @@ from . import _lib
 GAMMA_F32 = float(np.float32(0.99))
 
 
-def gae(reward, value, done, last_value=None, gamma=0.99, lam=0.95, adv=None, rtg=None):
+_GAE_ALGOS = {"auto": 0, "column": 1, "walk": 2, "scan": 3}
+
+
+def gae(reward, value, done, last_value=None, gamma=0.99, lam=0.95, adv=None, rtg=None, algo="auto"):
     """PPO.get_GAEs (PPO.py:193-203) over time-major [T, N] tensors.
 
     reward, value: f32 [T, N]; done: u8/bool [T, N]; last_value: f32 [N] or
     None (every segment end is an episode end).  Returns (adv, rtg) with
-    rtg = adv + value (PPO.py:46).  Bit-exact with the reference's fp32 order.
+    rtg = adv + value (PPO.py:46).  Bit-exact with the reference's fp32 order
+    for algo "auto" / "column" / "walk" (mm_gae_ex); "scan" reassociates the
+    recursion (parallel inside episodes, ~1e-7 relative).
     """
     T, N = value.shape
     r = reward.contiguous()
@@ -31,8 +36,8 @@ def gae(reward, value, done, last_value=None, gamma=0.99, lam=0.95, adv=None, rt
         rtg = torch.empty_like(v)
     g = float(np.float32(gamma))
     gl = float(np.float32(gamma * lam))  # python float product, cast once (PPO.py:201)
-    _lib.check(_lib.lib().mm_gae(_lib.ptr(r), _lib.ptr(v), _lib.ptr(d), _lib.ptr(lv), int(T), int(N), g, gl,
-                                 _lib.ptr(adv), _lib.ptr(rtg), _lib.stream_ptr()), "mm_gae")
+    _lib.check(_lib.lib().mm_gae_ex(_lib.ptr(r), _lib.ptr(v), _lib.ptr(d), _lib.ptr(lv), int(T), int(N), g, gl,
+                                    _lib.ptr(adv), _lib.ptr(rtg), _GAE_ALGOS[algo], _lib.stream_ptr()), "mm_gae_ex")
     return adv, rtg
 
 

@@ -35,26 +35,35 @@ def _split_episodes(r, v, d):
     return out
 
 
+@pytest.mark.parametrize("algo", ["auto", "column", "walk"])
 @pytest.mark.parametrize("T,N", [(1, 7), (16, 257), (64, 1000)])
-def test_gae_time_major_matches_oracle(T, N):
+def test_gae_time_major_matches_oracle(T, N, algo):
     rng = np.random.default_rng(T * 1000 + N)
     r = rng.choice(np.float32([0, 0, 0, 0.5, 1]), size=(T, N)).astype(np.float32)
     v = rng.normal(0, 1, (T, N)).astype(np.float32)
     d = rng.random((T, N)) < 0.1
-    adv, rtg = ops.gae(torch.as_tensor(r).cuda(), torch.as_tensor(v).cuda(), torch.as_tensor(d).cuda())
+    adv, rtg = ops.gae(torch.as_tensor(r).cuda(), torch.as_tensor(v).cuda(), torch.as_tensor(d).cuda(), algo=algo)
     assert np.array_equal(adv.cpu().numpy(), _split_episodes(r, v, d))
     assert np.array_equal(rtg.cpu().numpy(), adv.cpu().numpy() + v)
 
 
-def test_gae_bootstrap_and_scale():
-    T, N = 32, 65536  # configs: 65,536 mazes, T=32
-    rng = np.random.default_rng(0)
-    r = rng.choice(np.float32([0, 0.5, 1]), size=(T, N)).astype(np.float32)
-    v = rng.normal(0, 1, (T, N)).astype(np.float32)
-    d = rng.random((T, N)) < 0.02
-    lv = rng.normal(0, 1, N).astype(np.float32)
-    adv, _ = ops.gae(*(torch.as_tensor(x).cuda() for x in (r, v, d)), last_value=torch.as_tensor(lv).cuda())
-    # numpy fp32 emulation of the bootstrapped recursion
+def _long_episodes(rng, T, N, max_len=1200):
+    """done flags of whole episodes of 1 .. max_len steps (the reference's
+    episodes end by exit or by max_timestep truncation, maze.py:116-121)."""
+    d = np.zeros((T, N), bool)
+    for n in range(N):
+        t = -1
+        while True:
+            t += int(rng.integers(1, max_len + 1))
+            if t >= T:
+                break
+            d[t, n] = True
+    return d
+
+
+def _bootstrap_ref(r, v, d, lv):
+    """numpy fp32 emulation of the recursion with a bootstrap value V(s_T)."""
+    T, N = r.shape
     f = np.float32
     g, gl = f(0.99), f(0.99 * 0.95)
     a = np.zeros(N, np.float32)
@@ -67,7 +76,46 @@ def test_gae_bootstrap_and_scale():
         a = (delta + np.where(d[t], f(0), gl) * a).astype(np.float32)
         ref[t] = a
         vn, dn = v[t], d[t]
-    assert np.array_equal(adv.cpu().numpy(), ref)
+    return ref
+
+
+@pytest.mark.parametrize("T,N", [(15600, 1), (5000, 3), (700, 64)])
+def test_gae_long_episodes(T, N):
+    """Whole-episode batches (PPO.py:108-141: one maze, ~15,600 steps, episodes
+    up to max_timestep=1200): the episode-parallel walk is bit-identical to the
+    per-episode reference recursion; the shuffle scan is within 1e-5 of it."""
+    rng = np.random.default_rng(T + N)
+    r = rng.choice(np.float32([0, 0, 0, 0.5, 1, -0.25]), size=(T, N)).astype(np.float32)
+    v = rng.normal(0, 1, (T, N)).astype(np.float32)
+    d = _long_episodes(rng, T, N)
+    ref = _split_episodes(r, v, d)
+    tr, tv, td = (torch.as_tensor(x).cuda() for x in (r, v, d))
+    for algo in ("auto", "walk", "column"):
+        adv, rtg = ops.gae(tr, tv, td, algo=algo)
+        assert np.array_equal(adv.cpu().numpy(), ref), algo
+        assert np.array_equal(rtg.cpu().numpy(), ref + v), algo
+    adv, rtg = ops.gae(tr, tv, td, algo="scan")
+    scale = np.abs(ref).max(0, keepdims=True)
+    np.testing.assert_allclose(adv.cpu().numpy(), ref, rtol=1e-5, atol=(1e-5 * scale).max())
+    # a bootstrapped last fragment (the horizon cut) on the same data
+    lv = rng.normal(0, 1, N).astype(np.float32)
+    ref_b = _bootstrap_ref(r, v, d, lv)
+    for algo in ("walk", "column"):
+        adv, _ = ops.gae(tr, tv, td, last_value=torch.as_tensor(lv).cuda(), algo=algo)
+        assert np.array_equal(adv.cpu().numpy(), ref_b), algo
+    adv, _ = ops.gae(tr, tv, td, last_value=torch.as_tensor(lv).cuda(), algo="scan")
+    np.testing.assert_allclose(adv.cpu().numpy(), ref_b, rtol=1e-5, atol=1e-5 * np.abs(ref_b).max())
+
+
+def test_gae_bootstrap_and_scale():
+    T, N = 32, 65536  # configs: 65,536 mazes, T=32
+    rng = np.random.default_rng(0)
+    r = rng.choice(np.float32([0, 0.5, 1]), size=(T, N)).astype(np.float32)
+    v = rng.normal(0, 1, (T, N)).astype(np.float32)
+    d = rng.random((T, N)) < 0.02
+    lv = rng.normal(0, 1, N).astype(np.float32)
+    adv, _ = ops.gae(*(torch.as_tensor(x).cuda() for x in (r, v, d)), last_value=torch.as_tensor(lv).cuda())
+    assert np.array_equal(adv.cpu().numpy(), _bootstrap_ref(r, v, d, lv))
 
 
 def _random_masks(rng, M):
