@@ -93,7 +93,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mazes", type=int, default=65536, help="mazes per GPU")
+    ap.add_argument("--mazes", type=int, default=None,
+                    help="mazes per GPU (default 65,536; 32,768 = configs[4]'s 262,144 / 8 with --dtype f16)")
+    ap.add_argument("--dtype", choices=("f32", "f16"), default="f32",
+                    help="f32: the GEMMs at fp32-class accuracy (bf16x3 MFMA, the headline); f16: fp16 MFMA operands "
+                         "with fp32 accumulation and fp32 master weights (BASELINE configs[4])")
     ap.add_argument("--size", type=int, default=10, help="default_size (cells); layout is 2*size-1")
     ap.add_argument("--horizon", type=int, default=16, help="env-steps per maze per iteration")
     ap.add_argument("--max-t", type=int, default=1200, help="max_timestep (main.py:20)")
@@ -110,11 +114,13 @@ def main():
     if world != a.gpus and dp.rank == 0:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
+    if a.mazes is None:
+        a.mazes = 65536 if a.dtype == "f32" else 32768
     n, T = a.mazes, a.horizon
     samples_local = n * T
     batch_global = 5 * ((samples_local * world) // 5)
     agent = PPO(2, epochs=1, batch_size=batch_global, lr=1.4e-4, n_envs=n, horizon=T, load=False, verbose=False,
-                save=False, dp=dp, sample_seed=12345, tuned_gemms=not a.no_tuned_gemms,
+                save=False, dp=dp, sample_seed=12345, tuned_gemms=not a.no_tuned_gemms, dtype=a.dtype,
                 env_config=dict(default_size=(a.size, a.size), max_timestep=a.max_t, seed_base=0))
 
     def iteration():
@@ -177,12 +183,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": a.dtype,
         "data": "synthetic: procedurally generated mazes (CPython-MT seeds 0..N-1 per GPU), random-init "
                 "actor/critic (torch.manual_seed(3234)), actions sampled by the policy",
         "config": {
-            "workload": f"PPO rollout+GAE+update over {n} parallel {a.size}x{a.size} 2-agent mazes per GPU "
-                        f"(configs[1] loop at configs[2] scale)",
+            "workload": (f"PPO rollout+GAE+update over {n} parallel {a.size}x{a.size} 2-agent mazes per GPU "
+                         f"(configs[1] loop at configs[2] scale)") if a.dtype == "f32" else
+                        (f"PPO rollout+GAE+update over {n} parallel {a.size}x{a.size} 2-agent mazes per GPU, fp16 "
+                         f"actor/critic GEMMs, 6 logits (configs[4]: 262,144 mazes at 8 GPUs)"),
             "mazes_per_gpu": n, "maze": f"{a.size}x{a.size} (layout {H}x{H})", "max_timestep": a.max_t,
             "horizon": T, "global_batch": batch_global, "minibatch": batch_global // 5,
             "minibatch_steps_per_iter": minibatches_per_iter, "parallelism": f"dp{world}",

@@ -241,6 +241,35 @@ long mm_x3_mbits_len(int M);
 int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N, float* dy,
                     float* colsum, void* stream);
 
+/* Precision-generic forms of the actor/critic GEMMs (csrc/x3mlp.hip).
+ * prec MM_PREC_X3: bf16x3 operands (six products, fp32-class, as mm_x3_*);
+ * MM_PREC_F16: one fp16 plane per operand, one f16 MFMA per product, fp32
+ * accumulation (the fp16 actor/critic of BASELINE configs[4]; storage,
+ * master weights and optimizer stay fp32).  ascale / dscale multiply the A
+ * (dY) operand before its fp16 rounding and cscale the result (powers of two:
+ * exact; a gradient far below 1 keeps fp16 precision).  X3 requires 1.0 for
+ * all scales.
+ * mm_gemm_tp_len / mm_gemm_tp_pack: the TP form of B for that precision (P_F16:
+ * one 1-KiB plane per block).
+ * mm_gemm_nt: c = cscale (ascale A . B^T) (+ bias)(ReLU) -- mm_x3_nt_f32a's
+ * forward (mbits_out) and input-gradient (mbits_in, colsum) forms; A fp32
+ * [M, lda] with K, lda % 4 == 0 and 16-byte alignment, or (outputs N <= 64,
+ * e.g. the critic's [M, 130] observations) K, lda even and 8-byte alignment.
+ * mm_gemm_wgrad: the weight gradient of nn.Linear under autograd (networks.py
+ * :35-41, :87-106), dw [N, K] = cscale * sum_m (dscale dy[m, n]) x[m, k], dy
+ * [M, lddy], x [M, ldx], N <= 272; row slices' partials in ws
+ * [mm_gemm_wgrad_ws_len(M, N, K)] floats, summed in a fixed order. */
+#define MM_PREC_X3 0
+#define MM_PREC_F16 1
+long mm_gemm_tp_len(int prec, int R, int C);
+int mm_gemm_tp_pack(int prec, const float* X, int R, int C, int ld, int trans, uint16_t* tp, void* stream);
+int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
+               const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out, float* colsum, float cscale,
+               float* c, int ldc, void* stream);
+long mm_gemm_wgrad_ws_len(int M, int N, int K);
+int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
+                  float cscale, float* ws, float* dw, void* stream);
+
 /* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
  * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),
  * masks [2M, 6] u8, actions [2M, 2] i8 (move, mark); per sample the joint

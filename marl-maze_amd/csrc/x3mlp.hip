@@ -26,6 +26,22 @@
 // +7) reads the 16 bytes at l * 16 of a plane block: lane-linear, conflict
 // free, and exactly the image one global_load_lds_dwordx4 writes.
 // Padding rows / columns hold zeros (the packers and epilogues write them).
+//
+// Precision template P (MM_PREC_*): P_X3 is the above; P_F16 keeps ONE fp16
+// plane per operand (round-to-nearest), one f16 MFMA per product: the fp16
+// actor/critic of BASELINE configs[4].  Storage stays fp32 (activations,
+// gradients, master weights); an A-operand scale (a power of two, exact)
+// keeps small gradients out of the fp16 subnormal range and the epilogue
+// multiplies by its inverse (cscale).  The TP layout of P_F16 is the same
+// with one plane (1 KiB blocks).
+//
+// k_wgrad: the weight gradient dW [N, K] = sum_m dY[m, n] X[m, k] of every
+// nn.Linear in the update (networks.py:35-41, 87-106 under autograd).  The
+// reduction runs over the M rows, which both operands store row-major, so each
+// workgroup stages a 32-row step of dY and X into LDS already transposed into
+// fragment order (one thread: one column x 8 rows -> split -> 16-byte LDS
+// writes), waves own contiguous runs of output tiles (A fragments reused
+// along a run), and the row slices' partials are summed in a fixed order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,8 +54,16 @@ namespace x3 {
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
-constexpr int kBlk = 1536;  // uint16 per (rt, ks) block: 3 planes x 512
+enum { P_X3 = MM_PREC_X3, P_F16 = MM_PREC_F16 };
+template <int P>
+struct Prec {
+    static constexpr int kPlanes = P == P_X3 ? 3 : 1;
+    static constexpr int kBlk = 512 * kPlanes;  // uint16 per (rt, ks) block
+};
+
+constexpr int kBlk = 1536;  // uint16 per (rt, ks) block of P_X3: 3 planes x 512
 constexpr int kRowPad = 256;
 
 __host__ __device__ inline int rup(int x, int m) { return (x + m - 1) / m * m; }
@@ -71,8 +95,55 @@ __device__ __forceinline__ void split8(const float* v, uint4& h, uint4& m, uint4
     l = make_uint4(ll[0] | (ll[1] << 16), ll[2] | (ll[3] << 16), ll[4] | (ll[5] << 16), ll[6] | (ll[7] << 16));
 }
 
+// x * s -> fp16 (round to nearest even), two values packed
+__device__ __forceinline__ uint32_t f16x2_rn(float x0, float x1) {
+    typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+    const h2 h = __builtin_convertvector((__attribute__((ext_vector_type(2))) float){x0, x1}, h2);
+    return __builtin_bit_cast(uint32_t, h);
+}
+
+__device__ __forceinline__ uint4 f16x8_rn(const float* v, float s) {
+    return make_uint4(f16x2_rn(v[0] * s, v[1] * s), f16x2_rn(v[2] * s, v[3] * s), f16x2_rn(v[4] * s, v[5] * s),
+                      f16x2_rn(v[6] * s, v[7] * s));
+}
+
+// the 8 values of one fragment piece -> the P planes (16 bytes each) at dst, dst + 64, ... (uint4 units)
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l);
+
+template <int P>
+__device__ __forceinline__ void store_piece(const float* v, float s, uint4* dst) {
+    if constexpr (P == P_X3) {  // the hardware bf16 conversions (split2): ~4 VALU per value, not ~20
+        uint32_t h[4], m[4], l[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) split2(v[2 * k], v[2 * k + 1], h[k], m[k], l[k]);
+        dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
+        dst[64] = make_uint4(m[0], m[1], m[2], m[3]);
+        dst[128] = make_uint4(l[0], l[1], l[2], l[3]);
+    } else {
+        dst[0] = f16x8_rn(v, s);
+    }
+}
+
+// one fragment product, the precision's MFMAs (P_X3: the six partial products, small terms first)
+template <int P>
+__device__ __forceinline__ f32x4 mma(const bf16x8* a, const bf16x8* b, f32x4 acc) {
+    if constexpr (P == P_X3) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+    } else {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[0]), __builtin_bit_cast(f16x8, b[0]),
+                                                     acc, 0, 0, 0);
+    }
+    return acc;
+}
+
 // fp32 [R, C] (row-major, leading dimension ld; trans: element (i, j) at
 // X[j * ld + i]) -> TP.  One thread per (rt, ks, c, r) 8-element piece.
+template <int P>
 __global__ __launch_bounds__(256) void k_tp_pack(const float* __restrict__ X, int R, int C, int ld, int trans,
                                                  int nks, long total, uint16_t* __restrict__ tp) {
     for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -87,12 +158,7 @@ __global__ __launch_bounds__(256) void k_tp_pack(const float* __restrict__ X, in
             const int col = 32 * ks + kcol(c, j);
             v[j] = (row < R && col < C) ? (trans ? X[(size_t)col * ld + row] : X[(size_t)row * ld + col]) : 0.f;
         }
-        uint4 h, m, lo;
-        split8(v, h, m, lo);
-        uint4* dst = reinterpret_cast<uint4*>(tp + blk * kBlk) + l;
-        dst[0] = h;
-        dst[64] = m;
-        dst[128] = lo;
+        store_piece<P>(v, 1.f, reinterpret_cast<uint4*>(tp + blk * Prec<P>::kBlk) + l);
     }
 }
 
@@ -101,11 +167,11 @@ constexpr int kThreads = 64 * kWaves;
 constexpr int kBM = 16 * kWaves;  // rows per workgroup: one row tile per wave
 static_assert(kBM <= kRowPad, "A row blocks must stay inside the TP row padding");
 
-template <int NT>
+template <int NT, int P = P_X3>
 struct Cfg {
-    static constexpr int kPiecesB = 3 * NT;                     // 1-KiB B pieces per k-step
+    static constexpr int kPiecesB = Prec<P>::kPlanes * NT;      // 1-KiB B pieces per k-step
     static constexpr int kPerWaveB = (kPiecesB + kWaves - 1) / kWaves;
-    static constexpr int kStageB = NT * kBlk;                   // uint16 per B stage
+    static constexpr int kStageB = NT * Prec<P>::kBlk;          // uint16 per B stage
     static constexpr int kEpiLen = kWaves * 16 * 36 * 2;         // uint16: the waves' TP epilogue slices
     static constexpr int kLen0 = kStageB > kEpiLen ? kStageB : kEpiLen;  // stage buffer 0 doubles as epilogue
     static_assert((kLen0 + kStageB) * 2 <= 160 * 1024, "LDS");
@@ -127,12 +193,15 @@ struct Epi {
     uint16_t* ctp;           // TP of the output or null (needs one column block)
     float* colsum;           // EM_BWD, or null: per row tile column sums of the output [rows / 16][N]
     int ldc, ldm, relu, cnks;  // cnks = TP column blocks of the output (ceil(N / 32))
+    float cscale;              // P_F16: out = acc * cscale before bias (the inverse of the A scale)
 };
 
-// B piece i (column tile i / 3, plane i % 3) of k-step ks -> LDS (one 1-KiB LDS-DMA)
+// B piece i (column tile i / planes, plane i % planes) of k-step ks -> LDS (one 1-KiB LDS-DMA)
+template <int P>
 __device__ __forceinline__ void dma_b(const uint16_t* Bg, int nks, int ks, int i, uint16_t* dst, int lane) {
-    const int ct = i / 3, p = i - 3 * ct;
-    const uint4* src = reinterpret_cast<const uint4*>(Bg + ((size_t)ct * nks + ks) * kBlk + p * 512);
+    constexpr int np = Prec<P>::kPlanes;
+    const int ct = i / np, p = i - np * ct;
+    const uint4* src = reinterpret_cast<const uint4*>(Bg + ((size_t)ct * nks + ks) * Prec<P>::kBlk + p * 512);
     __builtin_amdgcn_global_load_lds(src + lane, dst, 16, 0, 0);
 }
 
@@ -156,7 +225,7 @@ struct ASrcTP {  // pre-split TP planes: three lane-linear 1-KiB loads
     typedef bf16x8 Raw[3];
     const uint16_t* A;  // the wave's row tile
     int nks;
-    __device__ void init(const uint16_t* base, int rt, int nks_, int, int, int) {
+    __device__ void init(const uint16_t* base, int rt, int nks_, int, int, int, float) {
         nks = nks_;
         A = base + (size_t)rt * nks * kBlk;
     }
@@ -165,52 +234,81 @@ struct ASrcTP {  // pre-split TP planes: three lane-linear 1-KiB loads
 #pragma unroll
         for (int q = 0; q < 3; q++) r[q] = __builtin_bit_cast(bf16x8, p[64 * q + lane]);
     }
+    template <int P>
     __device__ __forceinline__ void frag(const Raw& r, bf16x8 (&a)[3]) const {
+        static_assert(P == P_X3, "pre-split TP A operands are bf16x3");
 #pragma unroll
         for (int q = 0; q < 3; q++) a[q] = r[q];
     }
 };
 
-struct ASrcF32 {  // fp32 row-major [M, lda]: two 16-byte loads per lane, split in registers
+// fp32 row-major [M, lda]: VW = 4 (16-byte loads; lda % 4 == 0) or 2 (8-byte
+// loads: lda, K even, e.g. the critic's [M, 130] observations), split (P_X3)
+// or rounded after scaling (P_F16) in registers
+template <int VW>
+struct ASrcF32V {
     typedef float4 Raw[2];
-    const float* row;  // this lane's row (clamped inside the matrix), column 8 (l >> 4)
+    const float* row;  // this lane's row (clamped inside the matrix), column 4 (l >> 4)
     int K, ok;         // ok: the row exists
-    __device__ void init(const float* base, int rt, int, int M, int lda, int K_) {
+    float scale;
+    __device__ void init(const float* base, int rt, int, int M, int lda, int K_, float scale_) {
         const int lane = threadIdx.x & 63;
         const int r = 16 * rt + (lane & 15);
         ok = r < M;
         K = K_;
+        scale = scale_;
         row = base + (size_t)(ok ? r : 0) * lda + 4 * (lane >> 4);
     }
     __device__ __forceinline__ void load(int ks, Raw& r, int lane) const {
         const int k = 32 * ks + 4 * (lane >> 4);  // kcol(c, 0..3) = 4c.., kcol(c, 4..7) = 16 + 4c..
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        r[0] = (ok && k < K) ? *reinterpret_cast<const float4*>(row + 32 * ks) : z;
-        r[1] = (ok && k + 16 < K) ? *reinterpret_cast<const float4*>(row + 32 * ks + 16) : z;
+        if constexpr (VW == 4) {
+            r[0] = (ok && k < K) ? *reinterpret_cast<const float4*>(row + 32 * ks) : z;
+            r[1] = (ok && k + 16 < K) ? *reinterpret_cast<const float4*>(row + 32 * ks + 16) : z;
+        } else {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const float* p = row + 32 * ks + 16 * h;
+                const int kk = k + 16 * h;
+                const float2 a = (ok && kk < K) ? *reinterpret_cast<const float2*>(p) : make_float2(0.f, 0.f);
+                const float2 b = (ok && kk + 2 < K) ? *reinterpret_cast<const float2*>(p + 2) : make_float2(0.f, 0.f);
+                r[h] = make_float4(a.x, a.y, b.x, b.y);
+            }
+        }
     }
+    template <int P>
     __device__ __forceinline__ void frag(const Raw& r, bf16x8 (&a)[3]) const {
-        uint32_t h[4], m[4], l[4];
-        split2(r[0].x, r[0].y, h[0], m[0], l[0]);
-        split2(r[0].z, r[0].w, h[1], m[1], l[1]);
-        split2(r[1].x, r[1].y, h[2], m[2], l[2]);
-        split2(r[1].z, r[1].w, h[3], m[3], l[3]);
-        a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-        a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
-        a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+        if constexpr (P == P_X3) {
+            uint32_t h[4], m[4], l[4];
+            split2(r[0].x, r[0].y, h[0], m[0], l[0]);
+            split2(r[0].z, r[0].w, h[1], m[1], l[1]);
+            split2(r[1].x, r[1].y, h[2], m[2], l[2]);
+            split2(r[1].z, r[1].w, h[3], m[3], l[3]);
+            a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+            a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
+            a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+        } else {
+            const float s = scale;
+            a[0] = __builtin_bit_cast(bf16x8, make_uint4(f16x2_rn(r[0].x * s, r[0].y * s), f16x2_rn(r[0].z * s, r[0].w * s),
+                                                         f16x2_rn(r[1].x * s, r[1].y * s), f16x2_rn(r[1].z * s, r[1].w * s)));
+        }
     }
 };
+typedef ASrcF32V<4> ASrcF32;
+typedef ASrcF32V<2> ASrcF32U;
 
 // One k-step on stage buffer `cur`: split this step's A (raw -> fragments),
 // prefetch the next step's raw A (registers) and B pieces (the other buffer;
 // the DMA issues spread over the column loop), the 6 x NT MFMAs, one barrier.
-template <int NT, class AS>
+template <int NT, int P, class AS>
 __device__ __forceinline__ void k_step(f32x4 (&acc)[NT], const AS& as, const typename AS::Raw& raw,
                                        typename AS::Raw& rawn, const uint16_t* Bg, int nks, int ks,
                                        const uint16_t* cur, uint16_t* nxt, int wave, int lane) {
-    using C = Cfg<NT>;
+    using C = Cfg<NT, P>;
+    constexpr int np = Prec<P>::kPlanes;
     const bool more = ks + 1 < nks;
     bf16x8 a[3];
-    as.frag(raw, a);
+    as.template frag<P>(raw, a);
 #ifndef X3_NO_ALOAD  // diagnostic builds (tools/x3_variants.sh) only
     as.load(more ? ks + 1 : ks, rawn, lane);
 #endif
@@ -223,16 +321,12 @@ __device__ __forceinline__ void k_step(f32x4 (&acc)[NT], const AS& as, const typ
         if (false) {
 #endif
             const int i = wave + kWaves * c;
-            if (i < C::kPiecesB) dma_b(Bg, nks, ks + 1, i, nxt + i * 512, lane);
+            if (i < C::kPiecesB) dma_b<P>(Bg, nks, ks + 1, i, nxt + i * 512, lane);
         }
-        const bf16x8 bh = b8[(c * 3 + 0) * 64], bm = b8[(c * 3 + 1) * 64], bl = b8[(c * 3 + 2) * 64];
-        // small terms first
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], bh, acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bl, acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bm, acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], bh, acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bm, acc[c], 0, 0, 0);
-        acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], bh, acc[c], 0, 0, 0);
+        bf16x8 b[3];
+#pragma unroll
+        for (int q = 0; q < np; q++) b[q] = b8[(c * np + q) * 64];
+        acc[c] = mma<P>(a, b, acc[c]);
     }
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();  // vmcnt(0): this wave's next-stage pieces and A loads landed; the barrier: every
@@ -251,7 +345,7 @@ __device__ __forceinline__ void k_step(f32x4 (&acc)[NT], const AS& as, const typ
 // bytes of a row); no workgroup barrier.
 enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3 };
 
-template <int NT, int EM>
+template <int NT, int EM, int P>
 __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int M, int N, int col0, const Epi& ep,
                                              const float* sbias, int lane) {
     const int rq = 4 * (lane >> 4);  // first of this lane's four rows (within the tile)
@@ -272,6 +366,7 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
         for (int g = 0; g < 4; g++) {
             const int row = 16 * rt + rq + g, bit = 4 * c + g;
             float x = acc[c][g];
+            if (P == P_F16) x *= ep.cscale;
             if (EM == EM_BWD) {
                 if (!((bits[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
             } else {
@@ -288,7 +383,8 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
 #pragma unroll
             for (int g = 0; g < 4; g++) {
                 const int row = 16 * rt + rq + g;
-                if (row < M && ((bits[(4 * c + g) >> 5] >> ((4 * c + g) & 31)) & 1u)) cs += acc[c][g];
+                if (row < M && ((bits[(4 * c + g) >> 5] >> ((4 * c + g) & 31)) & 1u))
+                    cs += P == P_F16 ? acc[c][g] * ep.cscale : acc[c][g];
             }
             cs += __shfl_xor(cs, 16);
             cs += __shfl_xor(cs, 32);
@@ -360,10 +456,12 @@ __device__ __forceinline__ void epilogue_tp(const f32x4 (&acc)[NT], float* slice
 // DMA issues spread over the MFMA stream.  One barrier per k-step; four waves
 // per SIMD hide the LDS latency of the B fragment reads.  Persistent over
 // 256-row units.
-template <int NT, class AS, class AT, int EM>
-__global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int lda, const uint16_t* __restrict__ B,
-                                                   int M, int N, int K, int nks, int nrb, int ncb, Epi ep) {
-    using C = Cfg<NT>;
+template <int NT, int P, class AS, class AT, int EM>
+__global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int lda, float ascale,
+                                                   const uint16_t* __restrict__ B, int M, int N, int K, int nks,
+                                                   int nrb, int ncb, Epi ep) {
+    using C = Cfg<NT, P>;
+    static_assert(EM != EM_TP || P == P_X3, "TP outputs are bf16x3");
     // two distinct LDS objects: the compiler's alias scopes then let a B read of
     // one stage run while the DMA into the other is in flight
     __shared__ float sbias[16 * NT];  // the unit's bias columns (EM_F32 / EM_FWD); first: small LDS offsets
@@ -381,8 +479,8 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         if (rb >= nrb) continue;  // workgroup-uniform
         const int rt = rb * kWaves + wave;  // this wave's row tile
         AS as;
-        as.init(A, rt, nks, M, lda, K);
-        const uint16_t* Bg = B + (size_t)cb * NT * nks * kBlk;
+        as.init(A, rt, nks, M, lda, K, ascale);
+        const uint16_t* Bg = B + (size_t)cb * NT * nks * Prec<P>::kBlk;
         if (EM != EM_BWD && EM != EM_TP && ep.bias && threadIdx.x < 16 * NT) {  // visible after the prologue barrier
             int t = threadIdx.x;
             asm volatile("" : "+v"(t));  // recomputed per unit, not a loop-invariant address held (spilled) across it
@@ -395,23 +493,23 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         for (int c = 0; c < NT; c++) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         typename AS::Raw r0, r1;
-        for (int i = wave; i < C::kPiecesB; i += kWaves) dma_b(Bg, nks, 0, i, sB0 + i * 512, lane);
+        for (int i = wave; i < C::kPiecesB; i += kWaves) dma_b<P>(Bg, nks, 0, i, sB0 + i * 512, lane);
         as.load(0, r0, lane);
         __syncthreads();
         // k-steps in pairs so the two stage buffers are compile-time distinct
         // (no wait of a B fragment read on the other buffer's DMA)
         int ks = 0;
         for (; ks + 1 < nks; ks += 2) {
-            k_step<NT>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
-            k_step<NT>(acc, as, r1, r0, Bg, nks, ks + 1, sB1, sB0, wave, lane);
+            k_step<NT, P>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
+            k_step<NT, P>(acc, as, r1, r0, Bg, nks, ks + 1, sB1, sB0, wave, lane);
         }
-        if (ks < nks) k_step<NT>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
+        if (ks < nks) k_step<NT, P>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
 
         // ---- epilogue (after the last k-step's barrier both stage buffers are free) ----
-        if (EM == EM_TP)
+        if constexpr (EM == EM_TP)
             epilogue_tp<NT>(acc, reinterpret_cast<float*>(sB0) + wave * 16 * 36, rt, M, N, ep, lane);
         else
-            epilogue_f32<NT, EM>(acc, rt, M, N, cb * 16 * NT, ep, sbias, lane);
+            epilogue_f32<NT, EM, P>(acc, rt, M, N, cb * 16 * NT, ep, sbias, lane);
         // the next unit's DMA overwrites the epilogue slices: LDS reads done everywhere
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
@@ -483,6 +581,196 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz,
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Weight gradient (see the header): dW [N, K] = cscale * sum_m (dscale dY[m, n]) X[m, k].
+// Work unit = (row slice s, column block cb of <= 17 tiles); 8 waves; per
+// 32-row step every thread loads (operand, column, 8-row chunk) pieces for the
+// NEXT step into registers while the waves run the current step's MFMAs from
+// LDS; then it converts them into the fragment images (bf16x3 split or scaled
+// fp16) with one 16-byte LDS write per plane.  Wave w owns the contiguous run
+// of output tiles w * TPW .. (row-major over (n-tile, k-tile)), so its A
+// fragment is re-read only when the run crosses an n-tile.  Each unit writes
+// its partial [N, K] to ws[s]; mm_sum_leading sums the slices in order.
+// ---------------------------------------------------------------------------
+constexpr int kWgWaves = 8;
+constexpr int kWgThreads = 64 * kWgWaves;
+constexpr int kWgMaxT = 17;                                             // tiles per side of a unit
+constexpr int kWgPer = (64 * 2 * kWgMaxT + kWgThreads - 1) / kWgThreads;  // pieces per thread and step
+
+template <int P, int TPW>
+__global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ dy, int lddy, float dscale,
+                                                      const float* __restrict__ x, int ldx, int M, int N, int K,
+                                                      int TN, int NTK, int tpw, int rows, int nslices, int ncb,
+                                                      float cscale, float* __restrict__ ws) {
+    constexpr int kB = Prec<P>::kBlk;
+    constexpr int np = Prec<P>::kPlanes;
+    // two image sets [A: TN tiles | B: NTK tiles] (dynamic LDS): step st's MFMAs read set st & 1 while the
+    // waves convert step st + 1 into the other set -- one barrier per step
+    extern __shared__ __attribute__((aligned(16))) uint16_t img[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // XCD-aware: units u and u + 8 (one XCD) are the column blocks of one slice (its dY rows shared in L2)
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int s = (slot / ncb) * 8 + xcd, cb = slot % ncb;
+    if (s >= nslices) return;  // the whole workgroup
+    const int m_begin = s * rows, nrows = min(M, m_begin + rows) - m_begin;
+    const int col0 = cb * NTK * 16;
+    const int wA = TN * 16, wB = NTK * 16;  // staged columns per operand
+    const int itemsA = 4 * wA, items = itemsA + 4 * wB;  // itemsA = 64 TN: a piece's operand is wave-uniform
+    const int set = (TN + NTK) * kB;                     // uint16 per image set
+    const float* const baseA = dy + (size_t)m_begin * lddy;
+    const float* const baseB = x + (size_t)m_begin * ldx + col0;
+
+    // loop-invariant per piece q: first row inside a step (8c), element offset of (8c, column) from the
+    // operand's slice base, validity, and the LDS destination of its fragment piece
+    int r8[kWgPer], goff[kWgPer], loff[kWgPer];
+    bool ok[kWgPer];
+#pragma unroll
+    for (int q = 0; q < kWgPer; q++) {
+        const int e = threadIdx.x + kWgThreads * q;
+        const bool isA = e < itemsA;
+        const int e2 = isA ? e : e - itemsA, w = isA ? wA : wB;
+        const int c = e2 / w, j = e2 - c * w;  // 8-row chunk, column: consecutive threads, consecutive columns
+        ok[q] = e < items && (isA ? j < N : col0 + j < K);
+        r8[q] = 8 * c;
+        goff[q] = ok[q] ? 8 * c * (isA ? lddy : ldx) + j : 0;
+        loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
+    }
+
+    float raw[kWgPer][8];
+    auto load_piece = [&](int q, int r0) {  // rows r0 + 8c .. + 7 of the slice
+        const bool isA = threadIdx.x + kWgThreads * q < itemsA;  // wave-uniform
+        const int ld = isA ? lddy : ldx;
+        const float* rowp = (isA ? baseA : baseB) + (size_t)r0 * ld;  // uniform
+        int o = goff[q];
+        asm volatile("" : "+v"(o));  // per step: not 40 loop-invariant addresses held in registers
+        const int lim = nrows - r0 - r8[q];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#ifdef WG_NO_GLOAD  // diagnostic builds only: no global loads
+            raw[q][i] = ok[q] ? (float)(r0 + i) : 0.f;
+#else
+            raw[q][i] = (ok[q] && i < lim) ? rowp[o + i * ld] : 0.f;
+#endif
+        }
+    };
+    auto store_piece_q = [&](int q, uint16_t* dst_set) {
+        if (threadIdx.x + kWgThreads * q < items) {
+            const bool isA = threadIdx.x + kWgThreads * q < itemsA;
+            store_piece<P>(raw[q], isA ? dscale : 1.f, reinterpret_cast<uint4*>(dst_set + loff[q]));
+        }
+    };
+    auto lds_barrier = [&]() {  // LDS writes visible, no wait for the register prefetch (vmcnt)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; u++) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // wave w: the run of tiles w * tpw .. + tpw - 1 (row-major over (n-tile, k-tile)), balanced
+    const int ntiles = TN * NTK, first = wave * tpw, last = min(ntiles, first + tpw);
+    const int tn0 = first / NTK, tk0 = first - tn0 * NTK;
+    const int nsteps = (nrows + 31) / 32;
+#pragma unroll
+    for (int q = 0; q < kWgPer; q++) load_piece(q, 0);
+#pragma unroll
+    for (int q = 0; q < kWgPer; q++) store_piece_q(q, img);
+    if (nsteps > 1) {
+#pragma unroll
+        for (int q = 0; q < kWgPer; q++) load_piece(q, 32);
+    }
+    lds_barrier();
+    // the conversion of the next step's pieces is spread over the tile loop (VALU beside the MFMAs)
+    constexpr int kEvery = TPW >= kWgPer ? TPW / kWgPer : 1;
+    for (int st = 0; st < nsteps; st++) {
+        const uint16_t* cur = img + (st & 1) * set;
+        uint16_t* nxt = img + ((st + 1) & 1) * set;
+        const bool more = st + 1 < nsteps;
+        int tn = tn0, tk = tk0, curtn = -1;
+        bf16x8 a[3], b[3];
+#pragma unroll
+        for (int u = 0; u < TPW; u++) {
+#ifndef WG_NO_MFMA  // diagnostic builds only
+            if (first + u < last) {
+                if (tn != curtn) {
+                    curtn = tn;
+                    const bf16x8* pa = reinterpret_cast<const bf16x8*>(cur + tn * kB) + lane;
+#pragma unroll
+                    for (int q = 0; q < np; q++) a[q] = pa[64 * q];
+                }
+                const bf16x8* pb = reinterpret_cast<const bf16x8*>(cur + TN * kB + tk * kB) + lane;
+#pragma unroll
+                for (int q = 0; q < np; q++) b[q] = pb[64 * q];
+                acc[u] = mma<P>(a, b, acc[u]);
+            }
+            if (++tk == NTK) {
+                tk = 0;
+                tn++;
+            }
+#endif
+            if (more && u % kEvery == 0 && u / kEvery < kWgPer) store_piece_q(u / kEvery, nxt);
+        }
+        if (more) {
+#pragma unroll
+            for (int q = TPW / kEvery; q < kWgPer; q++) store_piece_q(q, nxt);  // (TPW < kWgPer)
+            if (st + 2 < nsteps) {
+#pragma unroll
+                for (int q = 0; q < kWgPer; q++) load_piece(q, 32 * (st + 2));  // a whole step ahead
+            }
+        }
+        lds_barrier();  // set st & 1 read by every wave, set (st + 1) & 1 written
+    }
+    float* out = ws + (size_t)s * N * K;
+    int tn = tn0, tk = tk0;
+#pragma unroll
+    for (int u = 0; u < TPW; u++) {
+        if (first + u < last) {
+            const int col = col0 + 16 * tk + (lane & 15);
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int row = 16 * tn + 4 * (lane >> 4) + g;
+                if (row < N && col < K) out[(size_t)row * K + col] = acc[u][g] * cscale;
+            }
+        }
+        if (++tk == NTK) {
+            tk = 0;
+            tn++;
+        }
+    }
+}
+
+// out[e] = sum over the row slices s of ws[s][e]: 16 groups of consecutive slices per element, each group's
+// loads all in flight (the plain per-element loop over S = 256 slices was latency-bound: ~90 us), the
+// groups then summed in order -- a fixed order, so the result is deterministic
+__global__ __launch_bounds__(256) void k_wg_reduce(const float* __restrict__ ws, int S, long n,
+                                                   float* __restrict__ out) {
+    __shared__ float red[16][17];
+    const int el = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const long e = blockIdx.x * 16L + el;
+    const int per = (S + 15) / 16, s0 = g * per, s1 = min(S, s0 + per);
+    float a = 0.f;
+    if (e < n) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = s0 + i < s1 ? ws[(long)(s0 + i) * n + e] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i++) a += v[i];
+        for (int t = s0 + 16; t < s1; t++) a += ws[(long)t * n + e];  // S > 256
+    }
+    red[g][el] = a;
+    __syncthreads();
+    if (g == 0 && e < n) {
+        float t = red[0][el];
+#pragma unroll
+        for (int k = 1; k < 16; k++) t += red[k][el];
+        out[e] = t;
+    }
+}
+
 }  // namespace x3
 }  // namespace mm
 
@@ -490,16 +778,33 @@ using namespace mm::x3;
 
 extern "C" long mm_x3_tp_len(int R, int C) { return (long)(rup(R, kRowPad) / 16) * (rup(C, 32) / 32) * kBlk; }
 
+extern "C" long mm_gemm_tp_len(int prec, int R, int C) {
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
+    return mm_x3_tp_len(R, C) / (prec == MM_PREC_X3 ? 1 : 3);
+}
+
 extern "C" long mm_x3_mbits_len(int M) { return (long)(rup(M, kRowPad) / 16) * 64 * kMaskWords; }
 
-extern "C" int mm_x3_tp_pack(const float* X, int R, int C, int ld, int trans, uint16_t* tp, void* stream) {
+extern "C" int mm_gemm_tp_pack(int prec, const float* X, int R, int C, int ld, int trans, uint16_t* tp,
+                               void* stream) {
     if (!X || !tp || R <= 0 || C <= 0 || ld < (trans ? R : C)) return MM_E_ARG;
     if ((uintptr_t)tp & 15) return MM_E_ARG;
     const int nks = rup(C, 32) / 32;
     const long total = (long)(rup(R, kRowPad) / 16) * nks * 64;
     const int grid = (int)std::min<long>((total + 255) / 256, 256L * 64);
-    hipLaunchKernelGGL(k_tp_pack, dim3(grid), dim3(256), 0, (hipStream_t)stream, X, R, C, ld, trans, nks, total, tp);
+    if (prec == MM_PREC_X3)
+        hipLaunchKernelGGL(k_tp_pack<P_X3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, X, R, C, ld, trans, nks,
+                           total, tp);
+    else if (prec == MM_PREC_F16)
+        hipLaunchKernelGGL(k_tp_pack<P_F16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, X, R, C, ld, trans, nks,
+                           total, tp);
+    else
+        return MM_E_ARG;
     return (int)hipGetLastError();
+}
+
+extern "C" int mm_x3_tp_pack(const float* X, int R, int C, int ld, int trans, uint16_t* tp, void* stream) {
+    return mm_gemm_tp_pack(MM_PREC_X3, X, R, C, ld, trans, tp, stream);
 }
 
 static int persistent_grid() {  // one 16-wave workgroup per CU
@@ -512,46 +817,64 @@ static int persistent_grid() {  // one 16-wave workgroup per CU
     return cus;
 }
 
-template <int NT, class AS, class AT>
-static int launch_nt(const AT* a, int lda, const uint16_t* b, int M, int N, int K, int ncb, const Epi& ep,
-                     hipStream_t s) {
+template <int NT, int P, class AS, class AT>
+static int launch_nt(const AT* a, int lda, float ascale, const uint16_t* b, int M, int N, int K, int ncb,
+                     const Epi& ep, hipStream_t s) {
     const int nks = rup(K, 32) / 32;
     const int nrb = rup(M, kBM) / kBM;
     const int grid = std::min(rup(nrb, 8) * ncb, persistent_grid());
     if (ep.ctp && ep.c) return MM_E_ARG;  // one output form per launch
-    if (ep.ctp)
-        hipLaunchKernelGGL((k_x3nt<NT, AS, AT, EM_TP>), dim3(grid), dim3(kThreads), 0, s, a, lda, b, M, N, K, nks, nrb,
-                           ncb, ep);
-    else if (ep.mbits_out)
-        hipLaunchKernelGGL((k_x3nt<NT, AS, AT, EM_FWD>), dim3(grid), dim3(kThreads), 0, s, a, lda, b, M, N, K, nks,
-                           nrb, ncb, ep);
+    if constexpr (P == P_X3) {
+        if (ep.ctp) {
+            hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_TP>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M,
+                               N, K, nks, nrb, ncb, ep);
+            return (int)hipGetLastError();
+        }
+    } else if (ep.ctp) {
+        return MM_E_ARG;
+    }
+    if (ep.mbits_out)
+        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_FWD>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M, N,
+                           K, nks, nrb, ncb, ep);
     else if (ep.mbits_in)
-        hipLaunchKernelGGL((k_x3nt<NT, AS, AT, EM_BWD>), dim3(grid), dim3(kThreads), 0, s, a, lda, b, M, N, K, nks,
-                           nrb, ncb, ep);
+        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_BWD>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M, N,
+                           K, nks, nrb, ncb, ep);
     else
-        hipLaunchKernelGGL((k_x3nt<NT, AS, AT, EM_F32>), dim3(grid), dim3(kThreads), 0, s, a, lda, b, M, N, K, nks,
-                           nrb, ncb, ep);
+        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_F32>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M, N,
+                           K, nks, nrb, ncb, ep);
     return (int)hipGetLastError();
 }
 
-template <class AS, class AT>
-static int dispatch_nt(const AT* a, int lda, const uint16_t* b_tp, int M, int N, int K, const Epi& ep,
+template <int P, class AS, class AT>
+static int dispatch_nt(const AT* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K, const Epi& ep,
                        hipStream_t s) {
     // column tiling: one block of <= 17 tiles, or several blocks of 15 (B rows are padded to 256)
     const int tiles = (N + 15) / 16;
     int NT, ncb;
-    if (tiles <= 4) { NT = 4; ncb = 1; }
+    if (tiles <= 1) { NT = 1; ncb = 1; }
+    else if (tiles <= 4) { NT = 4; ncb = 1; }
     else if (tiles <= 8) { NT = 8; ncb = 1; }
     else if (tiles <= 17) { NT = 17; ncb = 1; }
     else { NT = 15; ncb = (tiles + 14) / 15; }
     if (ncb * NT * 16 > rup(N, kRowPad)) return MM_E_ARG;  // B TP row padding would be overrun
     if (ep.ctp && ncb != 1) return MM_E_ARG;
     switch (NT) {
-        case 4: return launch_nt<4, AS>(a, lda, b_tp, M, N, K, ncb, ep, s);
-        case 8: return launch_nt<8, AS>(a, lda, b_tp, M, N, K, ncb, ep, s);
-        case 15: return launch_nt<15, AS>(a, lda, b_tp, M, N, K, ncb, ep, s);
-        default: return launch_nt<17, AS>(a, lda, b_tp, M, N, K, ncb, ep, s);
+        case 1: return launch_nt<1, P, AS>(a, lda, ascale, b_tp, M, N, K, ncb, ep, s);
+        case 4: return launch_nt<4, P, AS>(a, lda, ascale, b_tp, M, N, K, ncb, ep, s);
+        case 8: return launch_nt<8, P, AS>(a, lda, ascale, b_tp, M, N, K, ncb, ep, s);
+        case 15: return launch_nt<15, P, AS>(a, lda, ascale, b_tp, M, N, K, ncb, ep, s);
+        default: return launch_nt<17, P, AS>(a, lda, ascale, b_tp, M, N, K, ncb, ep, s);
     }
+}
+
+// 8-byte-row A sources serve only narrow outputs (the critic's first layer)
+template <int P>
+static int dispatch_nt_u(const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
+                         const Epi& ep, hipStream_t s) {
+    const int tiles = (N + 15) / 16;
+    if (tiles <= 1) return launch_nt<1, P, ASrcF32U>(a, lda, ascale, b_tp, M, N, K, 1, ep, s);
+    if (tiles <= 4) return launch_nt<4, P, ASrcF32U>(a, lda, ascale, b_tp, M, N, K, 1, ep, s);
+    return MM_E_ARG;
 }
 
 static int check_common(const uint16_t* b_tp, int M, int N, int K, const float* mask, int ldm, float* c, int ldc,
@@ -571,8 +894,32 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
     if (e) return e;
     if (!a_tp || ((uintptr_t)a_tp & 15)) return MM_E_ARG;
     if (M == 0) return 0;
-    Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32};
-    return dispatch_nt<ASrcTP>(a_tp, 0, b_tp, M, N, K, ep, (hipStream_t)stream);
+    Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32, 1.f};
+    return dispatch_nt<P_X3, ASrcTP>(a_tp, 0, 1.f, b_tp, M, N, K, ep, (hipStream_t)stream);
+}
+
+static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
+                        const float* bias, int relu, const float* mask, int ldm, const uint32_t* mbits_in,
+                        uint32_t* mbits_out, float* colsum, float cscale, float* c, int ldc, uint16_t* c_tp,
+                        void* stream) {
+    int e = check_common(b_tp, M, N, K, mask, ldm, c, ldc, c_tp);
+    if (e) return e;
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
+    if (prec == MM_PREC_X3 && (ascale != 1.f || cscale != 1.f)) return MM_E_ARG;  // the split is exact: no scaling
+    const bool v4 = !(K & 3) && !(lda & 3) && !((uintptr_t)a & 15);
+    const bool v2 = !(K & 1) && !(lda & 1) && !((uintptr_t)a & 7);
+    if (!a || lda < K || !(v4 || v2) || (!v4 && N > 64)) return MM_E_ARG;  // 8-byte rows: narrow outputs only
+    if ((mbits_in || mbits_out) && (N > 16 * 17 || c_tp || mask || (mbits_in && mbits_out))) return MM_E_ARG;
+    if (mbits_in && (bias || relu)) return MM_E_ARG;  // the input-gradient form: no bias, no ReLU of its own
+    if (colsum && (!mbits_in || !c)) return MM_E_ARG;
+    if (M == 0) return 0;
+    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale};
+    hipStream_t s = (hipStream_t)stream;
+    if (prec == MM_PREC_X3)
+        return v4 ? dispatch_nt<P_X3, ASrcF32>(a, lda, 1.f, b_tp, M, N, K, ep, s)
+                  : dispatch_nt_u<P_X3>(a, lda, 1.f, b_tp, M, N, K, ep, s);
+    return v4 ? dispatch_nt<P_F16, ASrcF32>(a, lda, ascale, b_tp, M, N, K, ep, s)
+              : dispatch_nt_u<P_F16>(a, lda, ascale, b_tp, M, N, K, ep, s);
 }
 
 // The same with A fp32 row-major [M, lda] (K % 4 == 0, lda % 4 == 0, 16-byte
@@ -580,15 +927,17 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
 extern "C" int mm_x3_nt_f32a(const float* a, int lda, const uint16_t* b_tp, int M, int N, int K, const float* bias,
                              int relu, const float* mask, int ldm, const uint32_t* mbits_in, uint32_t* mbits_out,
                              float* colsum, float* c, int ldc, uint16_t* c_tp, void* stream) {
-    int e = check_common(b_tp, M, N, K, mask, ldm, c, ldc, c_tp);
-    if (e) return e;
-    if (!a || (K & 3) || (lda & 3) || lda < K || ((uintptr_t)a & 15)) return MM_E_ARG;
-    if ((mbits_in || mbits_out) && (N > 16 * 17 || c_tp || mask || (mbits_in && mbits_out))) return MM_E_ARG;
-    if (mbits_in && (bias || relu)) return MM_E_ARG;  // the input-gradient form: no bias, no ReLU of its own
-    if (colsum && (!mbits_in || !c)) return MM_E_ARG;
-    if (M == 0) return 0;
-    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32};
-    return dispatch_nt<ASrcF32>(a, lda, b_tp, M, N, K, ep, (hipStream_t)stream);
+    if (!a || (K & 3) || (lda & 3) || ((uintptr_t)a & 15)) return MM_E_ARG;
+    return gemm_nt_f32a(MM_PREC_X3, a, lda, 1.f, b_tp, M, N, K, bias, relu, mask, ldm, mbits_in, mbits_out, colsum,
+                        1.f, c, ldc, c_tp, stream);
+}
+
+extern "C" int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
+                          const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out, float* colsum,
+                          float cscale, float* c, int ldc, void* stream) {
+    if (!c) return MM_E_ARG;
+    return gemm_nt_f32a(prec, a, lda, ascale, b_tp, M, N, K, bias, relu, nullptr, 0, mbits_in, mbits_out, colsum,
+                        cscale, c, ldc, nullptr, stream);
 }
 
 // dY = (dz W) * bits (the heads' backward through the last ReLU, bits from the
@@ -602,5 +951,94 @@ extern "C" int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uin
     const int nrt = (M + 15) / 16;
     hipLaunchKernelGGL(k_heads_bwd<17>, dim3((nrt + 3) / 4), dim3(256), 0, (hipStream_t)stream, dz, J, W, bits, M, N,
                        dy, colsum);
+    return (int)hipGetLastError();
+}
+
+// ---- weight gradient ----
+struct WgPlan {
+    int TN, NTK, ncb, nslices, rows, TPW, tpw;  // TPW: the instantiation (>= tpw, the balanced run length)
+};
+
+static WgPlan wg_plan(int prec, int M, int N, int K) {
+    WgPlan p;
+    p.TN = (N + 15) / 16;
+    const int tk_all = (K + 15) / 16;
+    // column blocks: at most 20 tiles per wave (the register budget of 2 waves per SIMD) and two image sets
+    // within 160 KiB of LDS; a slice's blocks share its dY rows through the XCD's L2
+    p.ncb = (tk_all + kWgMaxT - 1) / kWgMaxT;
+    const int kb = prec == MM_PREC_X3 ? 1536 : 512;
+    auto fits = [&](int ncb) {
+        const int ntk = (tk_all + ncb - 1) / ncb;
+        return p.TN * ntk <= kWgWaves * 20 && 2 * (p.TN + ntk) * kb * 2 <= 160 * 1024;
+    };
+    while (!fits(p.ncb)) p.ncb++;
+    p.NTK = (tk_all + p.ncb - 1) / p.ncb;
+    p.tpw = (p.TN * p.NTK + kWgWaves - 1) / kWgWaves;
+    static const int kTPW[] = {1, 2, 3, 5, 8, 12, 16, 20};
+    p.TPW = 0;
+    for (int t : kTPW)
+        if (t >= p.tpw) {
+            p.TPW = t;
+            break;
+        }
+    // about one unit per CU: slices of whole 32-row steps
+    const int want = std::max(1, std::min((M + 31) / 32, persistent_grid() / p.ncb));
+    p.rows = rup((M + want - 1) / want, 32);
+    p.nslices = std::max(1, (M + p.rows - 1) / p.rows);
+    return p;
+}
+
+extern "C" long mm_gemm_wgrad_ws_len(int M, int N, int K) {
+    if (M <= 0 || N <= 0 || K <= 0) return 0;
+    long n = 0;  // the larger of the two precisions' plans
+    for (int prec : {MM_PREC_X3, MM_PREC_F16}) {
+        const WgPlan p = wg_plan(prec, M, N, K);
+        n = std::max(n, (long)p.nslices * N * K);
+    }
+    return n;
+}
+
+template <int P>
+static int launch_wgrad(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
+                        int N, int K, float cscale, float* ws, hipStream_t s) {
+    const dim3 grid(rup(p.nslices, 8) * p.ncb), block(kWgThreads);
+    const size_t lds = (size_t)2 * (p.TN + p.NTK) * Prec<P>::kBlk * sizeof(uint16_t);
+#define MM_WG(T)                                                                                               \
+    case T:                                                                                                    \
+        {                                                                                                      \
+            static bool attr = false;                                                                          \
+            if (!attr) {                                                                                       \
+                if (hipFuncSetAttribute((const void*)k_wgrad<P, T>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                        160 * 1024) != hipSuccess)                                             \
+                    return MM_E_ARG;                                                                           \
+                attr = true;                                                                                   \
+            }                                                                                                  \
+        }                                                                                                      \
+        hipLaunchKernelGGL((k_wgrad<P, T>), grid, block, lds, s, dy, lddy, dscale, x, ldx, M, N, K, p.TN, p.NTK, \
+                           p.tpw, p.rows, p.nslices, p.ncb, cscale, ws);                                       \
+        break;
+    switch (p.TPW) {
+        MM_WG(1) MM_WG(2) MM_WG(3) MM_WG(5) MM_WG(8) MM_WG(12) MM_WG(16) MM_WG(20)
+        default: return MM_E_ARG;
+    }
+#undef MM_WG
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
+                             int K, float cscale, float* ws, float* dw, void* stream) {
+    if (!dw || M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
+    if (prec == MM_PREC_X3 && (dscale != 1.f || cscale != 1.f)) return MM_E_ARG;
+    hipStream_t s = (hipStream_t)stream;
+    if (M == 0) return (int)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)N * K, s);  // (empty inputs: no pointers)
+    if (!dy || !x || !ws) return MM_E_ARG;
+    const WgPlan p = wg_plan(prec, M, N, K);
+    if (!p.TPW) return MM_E_ARG;
+    const int e = prec == MM_PREC_X3 ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
+                                     : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    if (e) return e;
+    const long n = (long)N * K;
+    hipLaunchKernelGGL(k_wg_reduce, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, ws, p.nslices, n, dw);
     return (int)hipGetLastError();
 }

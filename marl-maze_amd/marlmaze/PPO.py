@@ -81,7 +81,7 @@ class PPO:
                  updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
                  seed=3234, sample_seed=None, device=None, model_path=MODEL_PATH, load=True, parity_mode=True,
                  bootstrap=True, dp=None, verbose=True, save=True, tuned_gemms=True, episode_batches=False,
-                 episode_chunk=64):
+                 episode_chunk=64, dtype="f32"):
         self.maze = None  # wired by Maze.__init__ (maze.py:39-42), as in the reference
         self.dp = dp if dp is not None else DP.single()
         if device is None:
@@ -97,8 +97,14 @@ class PPO:
         # its state is restored afterwards
         g = torch.random.get_rng_state()
         torch.default_generator.manual_seed(seed)
-        self.actor = Actor([264, 264, 264], parity_mode=parity_mode).to(self.device)
-        self.critic = Critic(agent_amount, hidden_sizes=[64, 64]).to(self.device)
+        # dtype "f32": the networks' GEMMs at fp32-class accuracy (bf16x3 MFMA); "f16": fp16 MFMA operands with
+        # fp32 accumulation, storage and Adam (BASELINE configs[4]); the parameters are fp32 either way
+        if dtype not in ("f32", "f16"):
+            raise ValueError(f"dtype must be 'f32' or 'f16', not {dtype!r}")
+        self.dtype = dtype
+        prec = "x3" if dtype == "f32" else "f16"
+        self.actor = Actor([264, 264, 264], parity_mode=parity_mode, gemm_prec=prec).to(self.device)
+        self.critic = Critic(agent_amount, hidden_sizes=[64, 64], gemm_prec=prec).to(self.device)
         torch.random.set_rng_state(g)
         self.dp.broadcast_params([self.actor, self.critic])
         # Adam (PPO.py:18-19); on the GPU the fused multi-tensor kernel (same update rule, one launch)

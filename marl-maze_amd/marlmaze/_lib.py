@@ -39,7 +39,10 @@ EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
-           "mm_sum_leading")
+           "mm_sum_leading", "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_wgrad_ws_len",
+           "mm_gemm_wgrad")
+
+PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 
 
 class EnvDesc(ctypes.Structure):
@@ -114,6 +117,16 @@ def lib():
         L.mm_ppo_loss_bwd.restype = i32
         L.mm_sum_leading.argtypes = [P, i32, ctypes.c_long, P, P, P]
         L.mm_sum_leading.restype = i32
+        L.mm_gemm_tp_len.argtypes = [i32, i32, i32]
+        L.mm_gemm_tp_len.restype = ctypes.c_long
+        L.mm_gemm_tp_pack.argtypes = [i32, P, i32, i32, i32, i32, P, P]
+        L.mm_gemm_tp_pack.restype = i32
+        L.mm_gemm_nt.argtypes = [i32, P, i32, f32, P, i32, i32, i32, P, i32, P, P, P, f32, P, i32, P]
+        L.mm_gemm_nt.restype = i32
+        L.mm_gemm_wgrad_ws_len.argtypes = [i32, i32, i32]
+        L.mm_gemm_wgrad_ws_len.restype = ctypes.c_long
+        L.mm_gemm_wgrad.argtypes = [i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P, P]
+        L.mm_gemm_wgrad.restype = i32
         L.mm_x3_mbits_len.argtypes = [i32]
         L.mm_x3_mbits_len.restype = ctypes.c_long
         L.mm_x3_nt_f32a.restype = i32

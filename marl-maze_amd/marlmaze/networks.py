@@ -14,6 +14,7 @@ so every embedding reads ``x[:, 0:d_i]`` and the actor sees only obs[0:4].
 feature its own slice (what the code evidently intended).
 """
 import ctypes
+import math
 import os as _os
 
 import numpy as np
@@ -152,29 +153,60 @@ def front_params(projection, attention):
             [attention.querys.weight, attention.keys.weight, attention.values.weight])
 
 
-# Large-M actor MLP (the 460 -> 264 -> 264 -> 264 ReLU trunk, networks.py:35-36)
-# runs on the x3 GEMMs of csrc/x3mlp.hip: fp32-class accuracy on the bf16 MFMA
-# (each operand split exactly into three bf16 parts, six products kept).  The
-# weights are packed once per call into fragment-order planes (tiny), the
-# activations stay fp32 row-major and are split inside the GEMM.  The forward
-# GEMMs record their ReLU masks as bits; the input-gradient GEMMs of the
-# backward apply them in their epilogue (no threshold_backward pass).  Weight
-# and bias gradients (reductions over all M rows) stay on the library
-# (split-K batched GEMM).  MARLMAZE_GEMM=lib keeps every GEMM on the library.
+# The actor MLP (the 460 -> 264 -> 264 -> 264 ReLU trunk + the two heads,
+# networks.py:35-41) and the critic (130 -> 64 -> 64 -> 1, networks.py:87-102)
+# run on the hand-written GEMMs of csrc/x3mlp.hip, forward and backward:
+# * precision "x3" (default): fp32-class -- each operand split exactly into
+#   three bf16 parts, six bf16 MFMA products kept; "f16": one fp16 MFMA product
+#   per element (BASELINE configs[4]).  Storage, master weights and Adam stay
+#   fp32 in both.
+# * weights are packed once per call into fragment-order planes (tiny); the
+#   activations stay fp32 row-major and are converted inside the GEMMs;
+# * the forward GEMMs record their ReLU masks as bits; the input-gradient GEMMs
+#   apply them in their epilogue (no threshold_backward pass) and emit the
+#   per-tile column sums of the next layer's bias gradient;
+# * weight gradients dW = dY^T X run on mm_gemm_wgrad (row-slice partials
+#   summed in a fixed order).
+# The fp16 backward GEMMs scale dY by 2^floor(log2 M): the losses are means
+# over M rows, so per-row gradients are ~1/M, and the scale keeps them in
+# fp16's normal range; the results are unscaled (powers of two: exact).
+# x3 below _X3_MIN_ROWS rows uses the fp32 library GEMMs instead (the same
+# accuracy class; small calls); MARLMAZE_GEMM=lib keeps every x3-precision
+# GEMM on the library.
 _X3_MIN_ROWS = 16384
+GEMM_PRECISIONS = ("x3", "f16")
+
+
+def _engine_ok(x, prec, widths):
+    if not x.is_cuda or x.dim() != 2 or x.stride(1) != 1 or any(n > 272 for n in widths):
+        return False
+    if prec == "x3":
+        return _os.environ.get("MARLMAZE_GEMM", "auto") != "lib" and x.shape[0] >= _X3_MIN_ROWS
+    return True  # f16: always (the library would compute in fp32)
 
 
 def _x3_ok(x, layers):
-    if _os.environ.get("MARLMAZE_GEMM", "auto") == "lib" or not x.is_cuda or x.dim() != 2:
-        return False
-    if x.shape[0] < _X3_MIN_ROWS or x.shape[1] % 4 or x.stride(1) != 1:
-        return False
-    return all(lin.weight.shape[0] <= 272 and lin.weight.shape[1] % 4 == 0 for lin in layers)
+    """The actor trunk's x3 condition (kept for the tests and tools)."""
+    return _engine_ok(x, "x3", [lin.weight.shape[0] for lin in layers]) and x.shape[1] % 4 == 0
+
+
+def _grad_scale(M, prec):
+    """The power-of-two dY scale of the fp16 backward GEMMs (1 for x3)."""
+    return float(2.0 ** int(math.floor(math.log2(max(int(M), 1))))) if prec == "f16" else 1.0
+
+
+def _wgrad(dy, x, prec):
+    """dW = dY^T X (mm_gemm_wgrad on the GPU)."""
+    if not dy.is_cuda:
+        return dy.t().mm(x)
+    from . import x3
+
+    return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=_grad_scale(dy.shape[0], prec))
 
 
 def _split_k_wgrad(dy, x):
-    """dW = dY^T X over M >> 10^5 rows as an S-way split-K batched GEMM (as one
-    GEMM the [out, in] result has too few tiles to fill 256 CUs)."""
+    """The library form of dW = dY^T X (hipBLASLt split-K batched GEMM + mm_sum_leading),
+    kept as the MARLMAZE_GEMM=lib path and for comparisons (tools/bench_wgrad.py)."""
     M = x.shape[0]
     S = 16 if M >= 16 * 4096 else 1
     if S == 1:
@@ -194,8 +226,8 @@ def _split_k_wgrad(dy, x):
     return out
 
 
-def _x3_trunk_fwd(h0, ws, bs, need_bits):
-    """The ReLU trunk on the x3 GEMMs; returns the activations [h0, h1, ...] and
+def _mlp_fwd(h0, ws, bs, prec, need_bits):
+    """The ReLU layers on the engine; returns the activations [h0, h1, ...] and
     the forward GEMMs' ReLU bit masks (None without need_bits)."""
     from . import x3
 
@@ -204,63 +236,78 @@ def _x3_trunk_fwd(h0, ws, bs, need_bits):
     h = h0
     for w, b in zip(ws, bs):
         mb = x3.mbits(M, dev) if need_bits else None
-        h, _ = x3.nt(h, x3.pack(w), bias=b, relu=True, mbits_out=mb)
+        h = x3.gemm(h, x3.pack(w, prec=prec), bias=b, relu=True, mbits_out=mb)
         hs.append(h)
         bits.append(mb)
     return hs, bits
 
 
-class _X3Trunk(torch.autograd.Function):
-    """The trunk alone with autograd (Actor.trunk under grad; the update uses
-    _X3Actor).  apply(h0, W0, b0, W1, b1, ...) -> h_last."""
+def _x3_trunk_fwd(h0, ws, bs, need_bits, prec="x3"):
+    return _mlp_fwd(h0, ws, bs, prec, need_bits)
+
+
+def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx):
+    """Backward through the ReLU layers given dY of the last one (already through
+    its ReLU) and that dY's per-tile column sums cs (None: sum dY itself).
+    Returns (dx or None, [dW0, db0, dW1, db1, ...])."""
+    from . import x3
+
+    L = len(ws)
+    s = _grad_scale(dy.shape[0], prec)
+    grads = [None] * (2 * L)
+    dx = None
+    for l in range(L - 1, -1, -1):
+        grads[2 * l] = _wgrad(dy, hs[l], prec)
+        grads[2 * l + 1] = dy.sum(0) if cs is None else cs.sum(0)
+        wt = x3.pack(ws[l], trans=True, prec=prec)
+        if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0): the ReLU bits of layer l-1's forward
+            cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
+            dy = x3.gemm(dy, wt, mbits_in=ctx_bits[l - 1], colsum=cs, ascale=s)
+        elif need_dx:
+            dx = x3.gemm(dy, wt, ascale=s)
+    return dx, grads
+
+
+class _EngineTrunk(torch.autograd.Function):
+    """The actor trunk alone with autograd (Actor.trunk under grad; the update
+    uses _EngineActor).  apply(prec, h0, W0, b0, W1, b1, ...) -> h_last."""
 
     @staticmethod
-    def forward(ctx, h0, *params):
-        hs, bits = _x3_trunk_fwd(h0, params[0::2], params[1::2], True)
+    def forward(ctx, prec, h0, *params):
+        hs, bits = _mlp_fwd(h0, params[0::2], params[1::2], prec, True)
         ctx.save_for_backward(*hs, *params[0::2])
-        ctx.bits = bits
+        ctx.bits, ctx.prec = bits, prec
         return hs[-1]
 
     @staticmethod
     def backward(ctx, dh):
-        from . import x3
-
         L = len(ctx.bits)
         saved = ctx.saved_tensors
         hs, ws = saved[:L + 1], saved[L + 1:]
-        grads = [None] * (2 * L)
         dy = torch.ops.aten.threshold_backward(dh.contiguous(), hs[L], 0)  # through the last ReLU
-        cs = None
-        dx = None
-        for l in range(L - 1, -1, -1):
-            grads[2 * l] = _split_k_wgrad(dy, hs[l])
-            grads[2 * l + 1] = dy.sum(0) if cs is None else cs.sum(0)
-            wt = x3.pack(ws[l], trans=True)
-            if l > 0:
-                cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
-                dy, _ = x3.nt(dy, wt, mbits_in=ctx.bits[l - 1], colsum=cs)
-            elif ctx.needs_input_grad[0]:
-                dx, _ = x3.nt(dy, wt)
-        return (dx, *grads)
+        dx, grads = _mlp_bwd(ctx.bits, hs, ws, dy, None, ctx.prec, ctx.needs_input_grad[1])
+        return (None, dx, *grads)
 
 
-class _X3Actor(torch.autograd.Function):
-    """The actor MLP on the x3 GEMMs: trunk (networks.py:35-36) + heads (:38-41).
-    apply(h0 [M, K0], Wh [J, K], bh [J], W0, b0, W1, b1, ...) -> logits [M, J].
+class _EngineActor(torch.autograd.Function):
+    """The actor MLP on the engine: trunk (networks.py:35-36) + heads (:38-41).
+    apply(prec, h0 [M, K0], Wh [J, K], bh [J], W0, b0, W1, b1, ...) -> logits [M, J].
 
     Backward: the heads' gradient goes through the last ReLU in one kernel
     (mm_x3_heads_bwd, using the last forward GEMM's ReLU bits); each
     input-gradient GEMM applies the ReLU bits of the layer below in its
-    epilogue and emits per-tile column sums (that layer's bias gradient); weight
-    gradients are split-K library GEMMs."""
+    epilogue and emits per-tile column sums (that layer's bias gradient);
+    weight gradients on mm_gemm_wgrad."""
 
     @staticmethod
-    def forward(ctx, h0, wh, bh, *params):
+    def forward(ctx, prec, h0, wh, bh, *params):
+        from . import x3
+
         ws, bs = params[0::2], params[1::2]
-        hs, bits = _x3_trunk_fwd(h0, ws, bs, True)
-        z = torch.addmm(bh, hs[-1], wh.t())
+        hs, bits = _mlp_fwd(h0, ws, bs, prec, True)
+        z = x3.gemm(hs[-1], x3.pack(wh, prec=prec), bias=bh)
         ctx.save_for_backward(*hs, wh, *ws)
-        ctx.bits = bits
+        ctx.bits, ctx.prec = bits, prec
         return z
 
     @staticmethod
@@ -271,21 +318,64 @@ class _X3Actor(torch.autograd.Function):
         saved = ctx.saved_tensors
         hs, wh, ws = saved[:L + 1], saved[L + 1], saved[L + 2:]
         dz = dz.contiguous()
-        dwh = _split_k_wgrad(dz, hs[L])
+        dwh = _wgrad(dz, hs[L], ctx.prec)
         dbh = dz.sum(0)
-        dy, cs = x3.heads_bwd(dz, wh, ctx.bits[L - 1])  # through the last ReLU
-        grads = [None] * (2 * L)
-        dx = None
-        for l in range(L - 1, -1, -1):
-            grads[2 * l] = _split_k_wgrad(dy, hs[l])
-            grads[2 * l + 1] = cs.sum(0)
-            wt = x3.pack(ws[l], trans=True)
-            if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0): the ReLU bits of layer l-1's forward
-                cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
-                dy, _ = x3.nt(dy, wt, mbits_in=ctx.bits[l - 1], colsum=cs)
-            elif ctx.needs_input_grad[0]:
-                dx, _ = x3.nt(dy, wt)
-        return (dx, dwh, dbh, *grads)
+        dy, cs = x3.heads_bwd(dz, wh, ctx.bits[L - 1])  # through the last ReLU (fp32)
+        dx, grads = _mlp_bwd(ctx.bits, hs, ws, dy, cs, ctx.prec, ctx.needs_input_grad[1])
+        return (None, dx, dwh, dbh, *grads)
+
+
+class _X3Trunk:
+    """_EngineTrunk at precision x3: apply(h0, W0, b0, ...)."""
+
+    @staticmethod
+    def apply(*args):
+        return _EngineTrunk.apply("x3", *args)
+
+
+class _X3Actor:
+    """_EngineActor at precision x3: apply(h0, Wh, bh, W0, b0, ...)."""
+
+    @staticmethod
+    def apply(*args):
+        return _EngineActor.apply("x3", *args)
+
+
+def _critic_fwd(x, params, prec, need_bits):
+    """networks.py:96-102 on the engine: x [M, 130] (8-byte rows) -> ReLU(64) ->
+    ReLU(64) -> V [M, 1]."""
+    from . import x3
+
+    w0, b0, w1, b1, w2, b2 = params
+    hs, bits = _mlp_fwd(x, (w0, w1), (b0, b1), prec, need_bits)
+    return x3.gemm(hs[-1], x3.pack(w2, prec=prec), bias=b2), hs, bits
+
+
+class _EngineCritic(torch.autograd.Function):
+    """The critic on the engine.  apply(prec, x [M, 130], W0, b0, W1, b1, W2, b2)
+    -> V [M, 1].  Backward: the value head through the last ReLU in one kernel
+    (mm_x3_heads_bwd, J = 1), the input-gradient GEMM through the first ReLU
+    (bits + bias-gradient column sums), weight gradients on mm_gemm_wgrad; no
+    gradient for the observations."""
+
+    @staticmethod
+    def forward(ctx, prec, x, *params):
+        v, hs, bits = _critic_fwd(x, params, prec, True)
+        ctx.save_for_backward(*hs, params[0], params[2], params[4])
+        ctx.bits, ctx.prec = bits, prec
+        return v
+
+    @staticmethod
+    def backward(ctx, dv):
+        from . import x3
+
+        x, h1, h2, w0, w1, w2 = ctx.saved_tensors
+        dv = dv.contiguous()
+        dw2 = _wgrad(dv, h2, ctx.prec)
+        db2 = dv.sum(0)
+        dy, cs = x3.heads_bwd(dv, w2, ctx.bits[1])  # (dV W2) * (h2 > 0)
+        _, grads = _mlp_bwd(ctx.bits, (x, h1), (w0, w1), dy, cs, ctx.prec, False)
+        return (None, None, *grads, dw2, db2)
 
 
 def _linear_fwd(x, w, b, relu):
@@ -326,9 +416,12 @@ def _linear(x, w, b, relu=False):
 class Actor(nn.Module):
     """networks.py:13-48.  forward(x) -> [move_logits [B,5], mark_logit [B,1]]."""
 
-    def __init__(self, hidden_sizes=(164, 164, 164, 164, 164), activation=nn.ReLU, parity_mode=True):
+    def __init__(self, hidden_sizes=(164, 164, 164, 164, 164), activation=nn.ReLU, parity_mode=True,
+                 gemm_prec="x3"):
         super().__init__()
         hidden_sizes = list(hidden_sizes)
+        assert gemm_prec in GEMM_PRECISIONS
+        self.gemm_prec = gemm_prec  # the MLP GEMMs' precision on the GPU (the front-end stays fp32)
         self.projection = Projection(parity_mode)
         self.attention = m_Attention()
         self.layers = nn.ModuleList()
@@ -360,10 +453,15 @@ class Actor(nn.Module):
         """[B, 6] = [5 move logits | mark logit] (both heads of networks.py:38-41)."""
         w, b = self.heads()
         h = self._front(x)
-        params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
-        if self.activation is nn.ReLU and _x3_ok(h, self.layers) and torch.is_grad_enabled() and (
-                h.requires_grad or any(p.requires_grad for p in params)):
-            return _X3Actor.apply(h, w, b, *params)  # trunk + heads, fused backward
+        if self._engine(h):
+            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            if torch.is_grad_enabled() and (h.requires_grad or any(p.requires_grad for p in params + [w, b])):
+                return _EngineActor.apply(self.gemm_prec, h, w, b, *params)  # trunk + heads, fused backward
+            from . import x3
+
+            with torch.no_grad():
+                hs, _ = _mlp_fwd(h, params[0::2], params[1::2], self.gemm_prec, False)
+                return x3.gemm(hs[-1], x3.pack(w, prec=self.gemm_prec), bias=b)
         return _linear(self._mlp(h), w, b)
 
     def trunk(self, x):
@@ -377,14 +475,18 @@ class Actor(nn.Module):
             return _FusedFront.apply(x, self.projection.parity_mode, *front_params(self.projection, self.attention))
         return self.attention(self.projection(x))  # host reference path (CPU tests only)
 
+    def _engine(self, h):
+        return (self.activation is nn.ReLU and _engine_ok(h, self.gemm_prec, [lin.weight.shape[0] for lin in self.layers])
+                and all(lin.weight.shape[1] % 4 == 0 for lin in self.layers))
+
     def _mlp(self, h):
         """The hidden layers (networks.py:35-36)."""
-        if self.activation is nn.ReLU and _x3_ok(h, self.layers):
+        if self._engine(h):
             params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
             if torch.is_grad_enabled() and (h.requires_grad or any(p.requires_grad for p in params)):
-                return _X3Trunk.apply(h, *params)
+                return _EngineTrunk.apply(self.gemm_prec, h, *params)
             with torch.no_grad():
-                hs, _ = _x3_trunk_fwd(h, params[0::2], params[1::2], False)
+                hs, _ = _mlp_fwd(h, params[0::2], params[1::2], self.gemm_prec, False)
             return hs[-1]
         if self.activation is nn.ReLU:
             for lin in self.layers:
@@ -399,9 +501,11 @@ class Actor(nn.Module):
 class Critic(nn.Module):
     """networks.py:84-106.  forward(x [.., agents, 65]) -> V [B, 1]."""
 
-    def __init__(self, agent_amount, hidden_sizes=(128, 128), activation=nn.ReLU):
+    def __init__(self, agent_amount, hidden_sizes=(128, 128), activation=nn.ReLU, gemm_prec="x3"):
         super().__init__()
         hidden_sizes = list(hidden_sizes)
+        assert gemm_prec in GEMM_PRECISIONS
+        self.gemm_prec = gemm_prec  # the GEMMs' precision on the GPU
         self.layers = nn.ModuleList()
         self.activation = activation
         self.agent_amount = agent_amount
@@ -418,6 +522,15 @@ class Critic(nn.Module):
     def forward(self, x):
         x = torch.as_tensor(x, dtype=torch.float32, device=self.layers[0].weight.device)
         x = x.reshape(-1, self.agent_amount * OBS_SPACE)
+        if (len(self.layers) == 3 and self.activation is nn.ReLU and x.shape[1] % 2 == 0
+                and all(lin.weight.shape[0] <= 64 for lin in self.layers)
+                and _engine_ok(x, self.gemm_prec, [lin.weight.shape[0] for lin in self.layers])):
+            x = x.contiguous()
+            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+                return _EngineCritic.apply(self.gemm_prec, x, *params)
+            with torch.no_grad():
+                return _critic_fwd(x, params, self.gemm_prec, False)[0]
         for lin in self.layers[:-1]:
             if self.activation is nn.ReLU:
                 x = _linear(x, lin.weight, lin.bias, relu=True)

@@ -1,20 +1,23 @@
-"""Python side of the pre-split x3 GEMMs (csrc/x3mlp.hip, include/marlmaze.h).
+"""Python side of the actor/critic GEMMs (csrc/x3mlp.hip, include/marlmaze.h).
 
 A TP tensor is the int16 buffer holding an fp32 [R, C] matrix as three exact
-bf16 planes in MFMA fragment order (R padded to 256, C to 32).  ``TP`` carries
-its logical shape.
+bf16 planes (precision "x3") or one fp16 plane ("f16") in MFMA fragment order
+(R padded to 256, C to 32).  ``TP`` carries its logical shape and precision.
 """
 import torch
 
 from . import _lib
 
 
-class TP:
-    __slots__ = ("buf", "R", "C")
+PRECS = {"x3": _lib.PREC_X3, "f16": _lib.PREC_F16}
 
-    def __init__(self, R, C, device, buf=None):
-        self.R, self.C = int(R), int(C)
-        n = _lib.lib().mm_x3_tp_len(self.R, self.C)
+
+class TP:
+    __slots__ = ("buf", "R", "C", "prec")
+
+    def __init__(self, R, C, device, buf=None, prec="x3"):
+        self.R, self.C, self.prec = int(R), int(C), prec
+        n = _lib.lib().mm_gemm_tp_len(PRECS[prec], self.R, self.C)
         self.buf = buf if buf is not None else torch.empty(n, dtype=torch.int16, device=device)
         assert self.buf.numel() >= n
 
@@ -22,14 +25,48 @@ class TP:
         return _lib.ptr(self.buf)
 
 
-def pack(x, out=None, trans=False):
+def pack(x, out=None, trans=False, prec="x3"):
     """fp32 [R, C] (or its transpose when trans=True, reading x as [C, R]) -> TP."""
     assert x.dtype == torch.float32 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
     R, C = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
-    out = out if out is not None else TP(R, C, x.device)
-    assert (out.R, out.C) == (R, C)
-    _lib.check(_lib.lib().mm_x3_tp_pack(_lib.ptr(x), R, C, x.stride(0), int(trans), out.ptr(), _lib.stream_ptr()),
-               "mm_x3_tp_pack")
+    out = out if out is not None else TP(R, C, x.device, prec=prec)
+    assert (out.R, out.C, out.prec) == (R, C, prec)
+    _lib.check(_lib.lib().mm_gemm_tp_pack(PRECS[prec], _lib.ptr(x), R, C, x.stride(0), int(trans), out.ptr(),
+                                          _lib.stream_ptr()), "mm_gemm_tp_pack")
+    return out
+
+
+def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None, ascale=1.0, out=None):
+    """out = (1/ascale) ((ascale A) B^T) (+bias)(ReLU) in B's precision (mm_gemm_nt):
+    A fp32 [M, K] row-major (16-byte rows, or 8-byte rows for N <= 64), B = TP
+    [N, K].  mbits_out records the ReLU mask; mbits_in applies one (the input
+    gradient through the ReLU below) with colsum its per-tile column sums.
+    ascale: a power of two for fp16 operands (1 for x3)."""
+    N, K = b.R, b.C
+    assert a.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1 and a.shape[1] == K, (a.shape, K)
+    M = a.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    _lib.check(_lib.lib().mm_gemm_nt(PRECS[b.prec], _lib.ptr(a), a.stride(0), float(ascale), b.ptr(), M, N, K,
+                                     _lib.ptr(bias), int(relu), _lib.ptr(mbits_in), _lib.ptr(mbits_out),
+                                     _lib.ptr(colsum), 1.0 / float(ascale), _lib.ptr(out), out.stride(0),
+                                     _lib.stream_ptr()), "mm_gemm_nt")
+    return out
+
+
+def wgrad(dy, x, prec="x3", dscale=1.0, out=None):
+    """dW [N, K] = dY^T X summed over the M rows (mm_gemm_wgrad), dY [M, N] and
+    X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and dy.stride(1) == 1 and x.stride(1) == 1
+    if out is None:
+        out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    L = _lib.lib()
+    ws = torch.empty(max(1, L.mm_gemm_wgrad_ws_len(M, N, K)), dtype=torch.float32, device=dy.device)
+    _lib.check(L.mm_gemm_wgrad(PRECS[prec], _lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M,
+                               N, K, 1.0 / float(dscale), _lib.ptr(ws), _lib.ptr(out), _lib.stream_ptr()),
+               "mm_gemm_wgrad")
     return out
 
 

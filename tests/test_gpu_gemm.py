@@ -1,0 +1,98 @@
+"""The precision-generic actor/critic GEMMs of csrc/x3mlp.hip against fp64.
+
+* mm_gemm_wgrad -- the weight gradient dW = dY^T X of every nn.Linear in the
+  update (networks.py:35-41, 87-106 under autograd), both precisions, every
+  shape the actor and critic use (incl. the column-blocked 264 x 460 and the
+  8-byte-row critic input [M, 130]).
+* mm_gemm_nt in fp16 (configs[4]) and on 8-byte rows (the critic's [M, 130]
+  observations), forward (bias + ReLU + bits) and input-gradient forms.
+
+Tolerances, relative to sum |a b| per output element (the bound any
+reordering of an fp32 sum obeys at ~n eps):
+  x3 (bf16x3, fp32-class): 1e-6 (measured 2-4e-7; the fp32 library GEMMs 3e-7);
+  f16 (one fp16 product, operands rounded to 11 bits): 2e-3 (two roundings of
+  2^-12 each, plus the fp32 sum).
+"""
+import pytest
+import torch
+
+from marlmaze import x3
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"x3": 1e-6, "f16": 2e-3}
+
+
+def _rel_err(got, ref, scale):
+    return ((got.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
+
+
+@pytest.mark.parametrize("prec", ["x3", "f16"])
+@pytest.mark.parametrize("M,N,K", [(419430, 264, 264), (70001, 264, 460), (40000, 6, 264), (209715, 64, 130),
+                                   (30000, 64, 64), (30000, 1, 64), (100, 264, 264), (1, 6, 264), (37, 5, 9)])
+def test_wgrad_matches_fp64(prec, M, N, K):
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    dy = torch.randn(M, N, device="cuda", generator=g)
+    x = torch.randn(M, K, device="cuda", generator=g)
+    dscale = 1.0
+    if prec == "f16":  # gradients of a mean over M rows are ~1/M: scaled into the fp16 normal range
+        dy *= 1.0 / M
+        dscale = float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
+    dw = x3.wgrad(dy, x, prec=prec, dscale=dscale)
+    ref = dy.double().t().mm(x.double())
+    scale = dy.double().abs().t().mm(x.double().abs())
+    err = _rel_err(dw, ref, scale)
+    assert dw.shape == (N, K) and err < TOL[prec], err
+    # deterministic: a fixed summation order
+    assert torch.equal(dw, x3.wgrad(dy, x, prec=prec, dscale=dscale))
+
+
+def test_wgrad_strided_and_empty():
+    """Row strides > width (a column slice of a wider buffer); M = 0 -> zeros."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    big = torch.randn(5000, 300, device="cuda", generator=g)
+    dy, x = big[:, :64], big[:, 100:230]
+    dw = x3.wgrad(dy, x)
+    ref = dy.double().t().mm(x.double())
+    assert _rel_err(dw, ref, dy.double().abs().t().mm(x.double().abs())) < 1e-6
+    z = x3.wgrad(torch.empty(0, 6, device="cuda"), torch.empty(0, 264, device="cuda"))
+    assert torch.equal(z, torch.zeros(6, 264, device="cuda"))
+
+
+@pytest.mark.parametrize("prec", ["x3", "f16"])
+@pytest.mark.parametrize("M,N,K", [(40000, 264, 460), (40000, 264, 264), (40000, 6, 264), (40000, 64, 130),
+                                   (40000, 1, 64), (777, 64, 64)])
+def test_gemm_forward_and_input_gradient(prec, M, N, K):
+    """Forward (bias + ReLU + bit mask) and the input-gradient form (bits of the
+    layer below, per-tile column sums) in both precisions, 16- and 8-byte rows."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) * 0.1
+    b = torch.randn(N, device="cuda", generator=g)
+    bits = x3.mbits(M, "cuda")
+    y = x3.gemm(a, x3.pack(w, prec=prec), bias=b, relu=True, mbits_out=bits)
+    pre = a.double() @ w.double().t() + b.double()
+    scale = a.double().abs() @ w.double().abs().t() + b.double().abs()
+    assert _rel_err(y, pre.clamp_min(0), scale) < TOL[prec]
+    # the bits record y > 0 exactly
+    w2 = torch.randn(48, N, device="cuda", generator=g) * 0.1  # the next layer's weight [out, in]
+    dy = torch.randn(M, 48, device="cuda", generator=g) / M
+    ascale = 1.0 if prec == "x3" else float(2.0 ** 16)
+    cs = x3.colsum_buf(M, N, "cuda")
+    dx = x3.gemm(dy, x3.pack(w2, trans=True, prec=prec), mbits_in=bits, colsum=cs, ascale=ascale)
+    ref = (dy.double() @ w2.double()) * (y > 0)
+    sc = dy.double().abs() @ w2.double().abs()
+    assert _rel_err(dx, ref, sc) < TOL[prec]
+    assert torch.equal(dx == 0, (y <= 0) | (dx == 0))
+    ref_cs = dx.double().sum(0)
+    assert ((cs.double().sum(0) - ref_cs).abs() <= 1e-5 * dx.double().abs().sum(0) + 1e-30).all()
+
+
+def test_gemm_rejects_bad_shapes():
+    from marlmaze import _lib
+
+    a = torch.randn(100, 130, device="cuda")
+    with pytest.raises(_lib.MMError):  # 8-byte rows: only narrow outputs
+        x3.gemm(a, x3.pack(torch.randn(264, 130, device="cuda")))
+    with pytest.raises(_lib.MMError):  # x3 operands are exact splits: no scaling
+        x3.gemm(torch.randn(100, 64, device="cuda"), x3.pack(torch.randn(8, 64, device="cuda")), ascale=2.0)
