@@ -743,6 +743,173 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
     }
 }
 
+// Structured form of k_wgrad for the shapes the actor and critic use (TN, NTK
+// compile-time): wave w owns the rectangle of n-tiles RN w .. RN w + RN - 1
+// by all NTK k-tiles (its RN A fragments held in registers, each B fragment
+// read once and used RN times, the next k-tile's B fragments read while the
+// current ones feed the MFMAs), plus its share of the leftover n-tiles
+// (TN - 8 RN rows of NTK tiles, dealt round-robin: A and B read per tile).
+// No runtime branch in the MFMA loop.  Staging, double-buffered images,
+// partials and the reduction are those of k_wgrad.
+template <int P, int TN, int NTK>
+__global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restrict__ dy, int lddy, float dscale,
+                                                           const float* __restrict__ x, int ldx, int M, int N, int K,
+                                                           int rows, int nslices, int ncb, float cscale,
+                                                           float* __restrict__ ws) {
+    constexpr int kB = Prec<P>::kBlk;
+    constexpr int np = Prec<P>::kPlanes;
+    constexpr int RN = TN / kWgWaves;                               // n-tiles per wave in the rectangle
+    constexpr int kRem = (TN - kWgWaves * RN) * NTK;                // leftover tiles
+    constexpr int EX = (kRem + kWgWaves - 1) / kWgWaves;            // leftover tiles per wave (max)
+    constexpr int kSet = (TN + NTK) * kB;                           // uint16 per image set
+    constexpr int itemsA = 64 * TN, items = itemsA + 64 * NTK;      // staged pieces per step
+    constexpr int kPer = (items + kWgThreads - 1) / kWgThreads;
+    extern __shared__ __attribute__((aligned(16))) uint16_t img[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int s = (slot / ncb) * 8 + xcd, cb = slot % ncb;
+    if (s >= nslices) return;  // the whole workgroup
+    const int m_begin = s * rows, nrows = min(M, m_begin + rows) - m_begin;
+    const int col0 = cb * NTK * 16;
+    const float* const baseA = dy + (size_t)m_begin * lddy;
+    const float* const baseB = x + (size_t)m_begin * ldx + col0;
+
+    int r8[kPer], goff[kPer], loff[kPer];
+    bool ok[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const int e = threadIdx.x + kWgThreads * q;
+        const bool isA = e < itemsA;
+        const int e2 = isA ? e : e - itemsA, w = isA ? 16 * TN : 16 * NTK;
+        const int c = e2 / w, j = e2 - c * w;
+        ok[q] = e < items && (isA ? j < N : col0 + j < K);
+        r8[q] = 8 * c;
+        goff[q] = ok[q] ? 8 * c * (isA ? lddy : ldx) + j : 0;
+        loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
+    }
+    float raw[kPer][8];
+    auto load_piece = [&](int q, int r0) {
+        const bool isA = threadIdx.x + kWgThreads * q < itemsA;  // wave-uniform (itemsA = 64 TN)
+        const int ld = isA ? lddy : ldx;
+        const float* rowp = (isA ? baseA : baseB) + (size_t)r0 * ld;
+        int o = goff[q];
+        asm volatile("" : "+v"(o));
+        const int lim = nrows - r0 - r8[q];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#ifdef WG_NO_GLOAD
+            raw[q][i] = ok[q] ? (float)(r0 + i) : 0.f;
+#else
+            raw[q][i] = (ok[q] && i < lim) ? rowp[o + i * ld] : 0.f;
+#endif
+        }
+    };
+    auto store_piece_q = [&](int q, uint16_t* dst_set) {
+        if (threadIdx.x + kWgThreads * q < items) {
+            const bool isA = threadIdx.x + kWgThreads * q < itemsA;
+            store_piece<P>(raw[q], isA ? dscale : 1.f, reinterpret_cast<uint4*>(dst_set + loff[q]));
+        }
+    };
+    auto lds_barrier = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto frag = [&](const uint16_t* tile, bf16x8 (&f)[3]) {
+        const bf16x8* p = reinterpret_cast<const bf16x8*>(tile) + lane;
+#pragma unroll
+        for (int q = 0; q < np; q++) f[q] = p[64 * q];
+    };
+
+    f32x4 acc[RN * NTK + EX];
+#pragma unroll
+    for (int u = 0; u < RN * NTK + EX; u++) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nsteps = (nrows + 31) / 32;
+#pragma unroll
+    for (int q = 0; q < kPer; q++) load_piece(q, 0);
+#pragma unroll
+    for (int q = 0; q < kPer; q++) store_piece_q(q, img);
+    if (nsteps > 1) {
+#pragma unroll
+        for (int q = 0; q < kPer; q++) load_piece(q, 32);
+    }
+    lds_barrier();
+    // conversion of the next step's pieces: piece q at slot q * kEvery of the tile loop (VALU beside the
+    // MFMAs), the rest after it
+    constexpr int kSlots = (RN > 0 ? NTK : 0) + EX;
+    constexpr int kEvery = kSlots >= kPer ? kSlots / kPer : 1;
+    // fp16 (cheap conversion, short MFMA phase): all after the MFMAs, so the loads issued at the end of the
+    // previous step get the whole MFMA phase to arrive (measured: 264 x 460 415 -> 366 us; x3: 765 -> 788)
+#if !defined(WG_NO_MFMA) && !defined(WG_CONV_LATE)
+    constexpr int kDone = P == P_F16 ? 0 : ((kSlots + kEvery - 1) / kEvery < kPer ? (kSlots + kEvery - 1) / kEvery : kPer);
+#else
+    constexpr int kDone = 0;
+#endif
+    for (int st = 0; st < nsteps; st++) {
+        const uint16_t* cur = img + (st & 1) * kSet;
+        uint16_t* nxt = img + ((st + 1) & 1) * kSet;
+        const bool more = st + 1 < nsteps;
+        auto conv_at = [&](int slot) {
+            if (kDone > 0 && more && slot % kEvery == 0 && slot / kEvery < kPer) store_piece_q(slot / kEvery, nxt);
+        };
+#ifndef WG_NO_MFMA
+        if constexpr (RN > 0) {
+            bf16x8 a[RN][3], b[2][3];
+#pragma unroll
+            for (int r = 0; r < RN; r++) frag(cur + (RN * wave + r) * kB, a[r]);
+            frag(cur + TN * kB, b[0]);
+#pragma unroll
+            for (int tk = 0; tk < NTK; tk++) {
+                if (tk + 1 < NTK) frag(cur + (TN + tk + 1) * kB, b[(tk + 1) & 1]);  // next k-tile, ahead
+#pragma unroll
+                for (int r = 0; r < RN; r++) acc[r * NTK + tk] = mma<P>(a[r], b[tk & 1], acc[r * NTK + tk]);
+                conv_at(tk);
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < EX; e++) {
+            int j = wave + kWgWaves * e;  // leftover tile j (clamped: a duplicate, not stored)
+            j = j < kRem ? j : kRem - 1;
+            const int tn = kWgWaves * RN + j / NTK, tk = j % NTK;
+            bf16x8 a1[3], b1[3];
+            frag(cur + tn * kB, a1);
+            frag(cur + (TN + tk) * kB, b1);
+            acc[RN * NTK + e] = mma<P>(a1, b1, acc[RN * NTK + e]);
+            conv_at((RN > 0 ? NTK : 0) + e);
+        }
+#endif
+        if (more) {
+#pragma unroll
+            for (int q = kDone; q < kPer; q++) store_piece_q(q, nxt);
+            if (st + 2 < nsteps) {
+#pragma unroll
+                for (int q = 0; q < kPer; q++) load_piece(q, 32 * (st + 2));
+            }
+        }
+        lds_barrier();
+    }
+    float* out = ws + (size_t)s * N * K;
+    auto put = [&](const f32x4& v, int tn, int tk) {
+        const int col = col0 + 16 * tk + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int row = 16 * tn + 4 * (lane >> 4) + g;
+            if (row < N && col < K) out[(size_t)row * K + col] = v[g] * cscale;
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < RN; r++)
+#pragma unroll
+        for (int tk = 0; tk < NTK; tk++) put(acc[r * NTK + tk], RN * wave + r, tk);
+#pragma unroll
+    for (int e = 0; e < EX; e++) {
+        const int j = wave + kWgWaves * e;
+        if (j < kRem) put(acc[RN * NTK + e], kWgWaves * RN + j / NTK, j % NTK);
+    }
+}
+
 // out[e] = sum over the row slices s of ws[s][e]: 16 groups of consecutive slices per element, each group's
 // loads all in flight (the plain per-element loop over S = 256 slices was latency-bound: ~90 us), the
 // groups then summed in order -- a fixed order, so the result is deterministic
@@ -1025,6 +1192,42 @@ static int launch_wgrad(const WgPlan& p, const float* dy, int lddy, float dscale
     return (int)hipGetLastError();
 }
 
+// the structured kernel for the (TN, NTK) blocks the actor and critic produce; 1 = no instantiation
+template <int P, int TN, int NTK>
+static int launch_rect_t(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
+                         int N, int K, float cscale, float* ws, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k_wgrad_rect<P, TN, NTK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return MM_E_ARG;
+        attr = true;
+    }
+    const size_t lds = (size_t)2 * (TN + NTK) * Prec<P>::kBlk * sizeof(uint16_t);
+    hipLaunchKernelGGL((k_wgrad_rect<P, TN, NTK>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s, dy,
+                       lddy, dscale, x, ldx, M, N, K, p.rows, p.nslices, p.ncb, cscale, ws);
+    return (int)hipGetLastError();
+}
+
+template <int P>
+static int launch_rect_p(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
+                         int N, int K, float cscale, float* ws, hipStream_t s) {
+#define MM_WR(a, b) \
+    if (p.TN == a && p.NTK == b) return launch_rect_t<P, a, b>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    MM_WR(17, 9) MM_WR(17, 8) MM_WR(1, 17) MM_WR(4, 9) MM_WR(4, 4) MM_WR(1, 4)
+#undef MM_WR
+    return 1;
+}
+
+static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int lddy, float dscale, const float* x,
+                             int ldx, int M, int N, int K, float cscale, float* ws, hipStream_t s) {
+#ifdef WG_GENERIC  // diagnostic builds: the generic kernel for every shape
+    return 1;
+#endif
+    return prec == MM_PREC_X3 ? launch_rect_p<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
+                              : launch_rect_p<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+}
+
 extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
                              int K, float cscale, float* ws, float* dw, void* stream) {
     if (!dw || M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
@@ -1035,10 +1238,12 @@ extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, 
     if (!dy || !x || !ws) return MM_E_ARG;
     const WgPlan p = wg_plan(prec, M, N, K);
     if (!p.TPW) return MM_E_ARG;
-    const int e = prec == MM_PREC_X3 ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
-                                     : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    int e = launch_wgrad_rect(prec, p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    if (e == 1) e = prec == MM_PREC_X3 ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
+                                       : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
     if (e) return e;
     const long n = (long)N * K;
+
     hipLaunchKernelGGL(k_wg_reduce, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, ws, p.nslices, n, dw);
     return (int)hipGetLastError();
 }

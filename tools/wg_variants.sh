@@ -6,12 +6,14 @@
 set -e
 mkdir -p tools/_var
 SRC=marl-maze_amd/csrc
-for v in BASE NO_MFMA NO_GLOAD NO_BOTH; do
+for v in BASE NO_MFMA NO_GLOAD NO_BOTH GENERIC CONV_LATE; do
   defs=""
   case $v in
     NO_MFMA) defs="-DWG_NO_MFMA";;
     NO_GLOAD) defs="-DWG_NO_GLOAD";;
     NO_BOTH) defs="-DWG_NO_MFMA -DWG_NO_GLOAD";;
+    GENERIC) defs="-DWG_GENERIC";;
+    CONV_LATE) defs="-DWG_CONV_LATE";;
   esac
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off $defs -I include -I $SRC \
     -o tools/_var/wg_$v.so $SRC/*.hip &
