@@ -185,7 +185,7 @@ int mm_gae(const float* reward, const float* value, const uint8_t* done, const f
  *   MM_GAE_SCAN    one workgroup per column, affine-map suffix scan with
  *                  wavefront shuffles -- parallel inside an episode,
  *                  reassociated fp32 (not bit-exact; ~1e-7 relative);
- *   MM_GAE_AUTO    COLUMN for N >= 16384 or short T, else WALK (bit-exact). */
+ *   MM_GAE_AUTO    COLUMN for N >= 256 or short T, else WALK (bit-exact). */
 #define MM_GAE_AUTO 0
 #define MM_GAE_COLUMN 1
 #define MM_GAE_WALK 2

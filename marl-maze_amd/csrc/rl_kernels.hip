@@ -473,7 +473,10 @@ extern "C" int mm_gae_ex(const float* reward, const float* value, const uint8_t*
     if (T == 0 || N == 0) return 0;
     const GaeArgs a{reward, value, done, last_value, T, N, gamma, gamma_lambda, adv, rtg};
     hipStream_t s = (hipStream_t)stream;
-    if (algo == MM_GAE_AUTO) algo = (N >= 16384 || T <= 2 * kGaeU) ? MM_GAE_COLUMN : MM_GAE_WALK;
+    // measured (tools/bench_gae.py): one lane per column wins from a few hundred columns up (T = 400, 4,096
+    // columns: 55 us vs 1.7 ms walked); below that the serial column of one lane is latency-bound and the
+    // episode-parallel walk wins (T = 15,600, 1 column: 0.49 vs 2.05 ms)
+    if (algo == MM_GAE_AUTO) algo = (N >= 256 || T <= 2 * kGaeU) ? MM_GAE_COLUMN : MM_GAE_WALK;
     if (algo == MM_GAE_COLUMN) {
         hipLaunchKernelGGL(k_gae, dim3((N + 255) / 256), dim3(256), 0, s, a);
     } else if (algo == MM_GAE_WALK) {
