@@ -333,6 +333,51 @@ constexpr int kOffG = 0, kOffD = 1380, kOffX = 1840;  // reduction phase
 constexpr int kSampleF = 1980;  // floats per sample (>= 1978 and >= 1932; multiple of 4)
 constexpr int kEFUnits = kTok * (kGd / 4);           // 345 (token, 4 rows of [g|dctx])
 
+// phase 4b of the backward: E/F (+= [g|dctx] x^T) and e/f (+= [g|dctx]) per token over the iteration's
+// samples; thread t owns units t and t + 256 (token u / 15, rows 4 (u % 15) ..), fixed order
+template <int kStride = kSampleF, int kG = kOffG, int kD = kOffD, int kX = kOffX>
+__device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, float (&ae)[2][4][4], float (&as)[2][4]) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int unit = threadIdx.x + u * kBwdThreads;
+        if (unit < kEFUnits) {
+            const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
+            const int off = r0 < kQkv ? kG + tk * kQkv + r0 : kD + tk * kEmb + (r0 - kQkv);
+            for (int gg = 0; gg < nrow; gg++) {
+                const float* sg = sm + gg * kStride;
+                const float4 gv = *reinterpret_cast<const float4*>(sg + off);
+                const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
+                const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    ae[u][a][0] = fmaf(gr[a], xq.x, ae[u][a][0]);
+                    ae[u][a][1] = fmaf(gr[a], xq.y, ae[u][a][1]);
+                    ae[u][a][2] = fmaf(gr[a], xq.z, ae[u][a][2]);
+                    ae[u][a][3] = fmaf(gr[a], xq.w, ae[u][a][3]);
+                    as[u][a] += gr[a];
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void ef_write(float* partial, const float (&ae)[2][4][4], const float (&as)[2][4]) {
+    float* out = partial + (size_t)blockIdx.x * kPartLen;
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+        const int unit = threadIdx.x + u * kBwdThreads;
+        if (unit < kEFUnits) {
+            const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                *reinterpret_cast<float4*>(out + kPEF + (tk * kGd + r0 + a) * kPin) =
+                    make_float4(ae[u][a][0], ae[u][a][1], ae[u][a][2], ae[u][a][3]);
+                out[kPef + tk * kGd + r0 + a] = as[u][a];
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __restrict__ ws,
                                                               const float* __restrict__ x, int ldx, int B,
                                                               int parity, const float* __restrict__ dh,
@@ -468,44 +513,349 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
             *reinterpret_cast<float4*>(my + kOffX + i * kPin) = xv;
         }
         __syncthreads();
-        // phase 4b: E/F (+= [g|dctx] x^T) and e/f (+= [g|dctx]) per token
+        ef_accumulate(sm, nrow, ae, as);
+    }
+    ef_write(partial, ae, as);
+}
+
+// ---------------------------------------------------------------------------
+// backward on the MFMA (k_front_bwd_mfma): the per-sample attention products
+// run as 16x16x16 bf16 MFMA tiles with the exact three-way split (six products
+// per fp32 product, as csrc/x3mlp.hip), tokens padded 23 -> 32, d_k 10 -> 16,
+// d_v 20 -> 32.  One wavefront per sample (two samples per wave per
+// iteration).  Accumulator tiles feed the next products directly: a C tile
+// (lane l holds rows 4 (l >> 4) + g, column l & 15) is the B operand of a
+// 16x16x16 MFMA whose k runs over its rows, and its transpose is an A
+// operand -- so
+//   S   = Q K^T          (A: Q rows, B: K rows; computed in-lane)
+//   dP  = dctx V^T       (A: dctx rows from dh, B: V rows in-lane)
+//   dV^T = dctx^T P      (B = the P tiles themselves)
+//   dK^T = Q^T dS        (B = the dS tiles)
+//   dQ  = dS K           (A = dS re-read through a 4-KiB LDS transpose)
+// and every q/k/v operand value is formed in the lane that needs it from the
+// folded maps (4 FMAs each).  Softmax and dS = P (dP - rowsum(P dP)) / sqrt(10)
+// act on the C tiles (row reductions across 16 lanes).  The per-token
+// gradients g = [dq | dk | dv], dctx and x go to the same LDS rows as in
+// k_front_bwd, whose E/F accumulation phase follows unchanged.
+//
+// Measured (tools/bench_front.py, 419,430 rows; tools/pmc_front.sh): 2.70 ms
+// against k_front_bwd's 1.85 ms, so it is not the default.  It executes 2,196
+// VALU instructions per sample against the VALU kernel's 1,213: the exact
+// three-way split of every operand value (~700 per sample) and the 32 x 32
+// padding of the 23 x 23 attention (softmax and dS on 1,024 entries instead
+// of 529) cost more VALU than the 168 MFMAs per sample save.
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+// 4 fp32 -> three bf16 planes (x = hi + mid + lo exactly), hardware RNE conversions
+__device__ __forceinline__ void split4(const float* v, s16x4 (&p)[3]) {
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    uint32_t h[2], m[2], l[2];
 #pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int unit = threadIdx.x + u * kBwdThreads;
-            if (unit < kEFUnits) {
-                const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
-                const int off = r0 < kQkv ? kOffG + tk * kQkv + r0 : kOffD + tk * kEmb + (r0 - kQkv);
-                for (int gg = 0; gg < nrow; gg++) {
-                    const float* sg = sm + gg * kSampleF;
-                    const float4 gv = *reinterpret_cast<const float4*>(sg + off);
-                    const float4 xq = *reinterpret_cast<const float4*>(sg + kOffX + tk * kPin);
-                    const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
+    for (int k = 0; k < 2; k++) {
+        const float x0 = v[2 * k], x1 = v[2 * k + 1];
+        h[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){x0, x1}, bf2));
+        const float r0 = x0 - __uint_as_float(h[k] << 16), r1 = x1 - __uint_as_float(h[k] & 0xFFFF0000u);
+        m[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){r0, r1}, bf2));
+        const float s0 = r0 - __uint_as_float(m[k] << 16), s1 = r1 - __uint_as_float(m[k] & 0xFFFF0000u);
+        l[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){s0, s1}, bf2));
+    }
+    p[0] = __builtin_bit_cast(s16x4, make_uint2(h[0], h[1]));
+    p[1] = __builtin_bit_cast(s16x4, make_uint2(m[0], m[1]));
+    p[2] = __builtin_bit_cast(s16x4, make_uint2(l[0], l[1]));
+}
+
+// acc += A B over one k-block of 16 (fp32-class: the six partial products >= 2^-16 |ab|, small terms first)
+__device__ __forceinline__ f32x4_t mma16x3(const s16x4 (&a)[3], const s16x4 (&b)[3], f32x4_t acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[0], acc, 0, 0, 0);
+    return acc;
+}
+
+constexpr int kMmaPitch = 32;  // dS transpose buffer row pitch (floats)
+constexpr int kMG = 0, kMD = kTok * kQkv, kMX = kMD + kTok * kEmb;  // reduction operands per sample
+constexpr int kMmaSample = kMX + kTok * kPin;                       // 1,472 floats (>= the 32 x 32 transpose)
+static_assert(kMmaSample >= 32 * kMmaPitch, "the dS transpose lives in the sample's region");
+
+__global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd_mfma(const float* __restrict__ ws,
+                                                                   const float* __restrict__ x, int ldx, int B,
+                                                                   int parity, const float* __restrict__ dh,
+                                                                   float* __restrict__ partial) {
+    // per sample: the reduction operands G [23][40] | dctx [23][20] | x [23][4] (the first 1,024 floats
+    // serve as the sample's dS transpose buffer before G is written); the folded maps A | c staged once
+    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kMmaSample];
+    __shared__ __attribute__((aligned(16))) float tA[kTok * kQkv * kPin];
+    __shared__ __attribute__((aligned(16))) float tC[kTok * kQkv];
+    {
+        constexpr int kN = kTok * kQkv * kPin + kTok * kQkv, kPer = (kN + kBwdThreads - 1) / kBwdThreads;
+        float v[kPer];
 #pragma unroll
-                    for (int a = 0; a < 4; a++) {
-                        ae[u][a][0] = fmaf(gr[a], xq.x, ae[u][a][0]);
-                        ae[u][a][1] = fmaf(gr[a], xq.y, ae[u][a][1]);
-                        ae[u][a][2] = fmaf(gr[a], xq.z, ae[u][a][2]);
-                        ae[u][a][3] = fmaf(gr[a], xq.w, ae[u][a][3]);
-                        as[u][a] += gr[a];
+        for (int u = 0; u < kPer; u++) {
+            const int e = threadIdx.x + kBwdThreads * u;
+            v[u] = e < kN ? ws[e < kTok * kQkv * kPin ? kWsA + e : kWsC + e - kTok * kQkv * kPin] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            const int e = threadIdx.x + kBwdThreads * u;
+            if (e < kTok * kQkv * kPin) tA[e] = v[u];
+            else if (e < kN) tC[e - kTok * kQkv * kPin] = v[u];
+        }
+    }
+    const int wave = threadIdx.x >> 6;
+    float ae[2][4][4], as[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int a = 0; a < 4; a++) ae[u][a][0] = ae[u][a][1] = ae[u][a][2] = ae[u][a][3] = as[u][a] = 0.f;
+    const float* const fA = tA;  // folded maps [23][40][4] (LDS)
+    const float* const fC = tC;  // [23][40]
+    // output r (0-9 q, 10-19 k, 20-39 v) of token t for input slice xv; 0 for padding tokens
+    auto qkv = [&](int t, int r, float4 xv) -> float {
+        if (t >= kTok) return 0.f;
+        const float4 w = *reinterpret_cast<const float4*>(fA + (t * kQkv + r) * kPin);
+        float acc = w.x * xv.x;
+        acc = fmaf(w.y, xv.y, acc);
+        acc = fmaf(w.z, xv.z, acc);
+        acc = fmaf(w.w, xv.w, acc);
+        return acc + fC[t * kQkv + r];
+    };
+    const int iters = (B + kBwdRows - 1) / kBwdRows;
+    for (int it = blockIdx.x; it < iters; it += gridDim.x) {
+        const int row0 = it * kBwdRows;
+        const int nrow = min(kBwdRows, B - row0);
+        __syncthreads();  // previous iteration's reduction readers are done
+#pragma unroll 1
+        for (int half = 0; half < 2; half++) {
+            const int slot = 2 * wave + half;  // this wave's sample of the iteration
+            if (slot >= nrow) break;           // wave-uniform
+            // lane indices recomputed per sample behind an opaque copy: otherwise the compiler hoists every
+            // lane-dependent table address out of the loop and spills them
+            int lane = threadIdx.x & 63;
+            asm volatile("" : "+v"(lane));
+            const int c16 = lane & 15, q4 = lane >> 4;
+            const int row = row0 + slot;
+            const float* xr = x + (size_t)row * ldx;
+            const float* dhr = dh + (size_t)row * kRowF;
+            float* my = sm + slot * kMmaSample;
+            float* const tbuf = my;  // dS transpose (dead before G is written: one wave, LDS in program order)
+            // the 23 token input slices -> the sample's X rows (also the reduction's operand), then every
+            // q/k/v value reads its slice from LDS
+            const float* const X = my + kMX;
+            if (lane < kTok) *reinterpret_cast<float4*>(my + kMX + lane * kPin) = xslice(xr, lane, parity != 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            auto xk = [&](int tok) {
+                return tok < kTok ? *reinterpret_cast<const float4*>(X + tok * kPin) : make_float4(0.f, 0.f, 0.f, 0.f);
+            };
+            float4 xrow[2] = {xk(c16), xk(c16 + 16)};
+            // ---- S = Q K^T (d_k 10 -> one k-block of 16) ----
+            s16x4 aq[2][3], bk[2][3];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                float v[4], w[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int k = 4 * q4 + e;
+                    v[e] = k < kKq ? qkv(c16 + 16 * t, k, xrow[t]) : 0.f;
+                    w[e] = k < kKq ? qkv(c16 + 16 * t, kKq + k, xrow[t]) : 0.f;
+                }
+                split4(v, aq[t]);
+                split4(w, bk[t]);
+            }
+            f32x4_t P[2][2];
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++) P[ti][tj] = mma16x3(aq[ti], bk[tj], f32x4_t{0.f, 0.f, 0.f, 0.f});
+            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
+            // ---- dP = dctx V^T (d_v 20 -> two k-blocks); dS later overwrites it in place ----
+            f32x4_t dP[2][2];
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++) dP[ti][tj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kb = 0; kb < 2; kb++) {
+                const int d0 = 16 * kb + 4 * q4;  // this lane's 4 d's
+                s16x4 ad[2][3], bv[2][3];
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int tok = c16 + 16 * t;
+                    float v[4] = {0.f, 0.f, 0.f, 0.f}, w[4];
+                    if (tok < kTok && d0 < kEmb) {
+                        const float4 d4 = *reinterpret_cast<const float4*>(dhr + tok * kEmb + d0);
+                        v[0] = d4.x; v[1] = d4.y; v[2] = d4.z; v[3] = d4.w;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; e++) w[e] = d0 + e < kEmb ? qkv(tok, 2 * kKq + d0 + e, xrow[t]) : 0.f;
+                    split4(v, ad[t]);
+                    split4(w, bv[t]);
+                }
+#pragma unroll
+                for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++) dP[ti][tj] = mma16x3(ad[ti], bv[tj], dP[ti][tj]);
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
+            // ---- softmax rows (the reference's order: / sqrt(10), exp(x - max), * (1 / sum)) and dS ----
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++) {
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const bool rowok = 16 * ti + 4 * q4 + g < kTok;
+                    float s[2];
+                    float mx = -INFINITY;
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++) {
+                        s[tj] = (16 * tj + c16 < kTok) ? div_sqrt_kq(P[ti][tj][g]) : -INFINITY;
+                        mx = fmaxf(mx, s[tj]);
+                    }
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+                    float sum = 0.f;
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++) {
+                        s[tj] = (16 * tj + c16 < kTok) ? expf(s[tj] - mx) : 0.f;
+                        sum += s[tj];
+                    }
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 16);
+                    const float inv = 1.f / sum;
+                    float rs = 0.f;
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++) {
+                        const float p = rowok ? s[tj] * inv : 0.f;
+                        P[ti][tj][g] = p;
+                        rs = fmaf(dP[ti][tj][g], p, rs);
+                    }
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) rs += __shfl_xor(rs, o, 16);
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++)
+                        dP[ti][tj][g] = div_sqrt_kq(P[ti][tj][g] * (dP[ti][tj][g] - rs));  // = dS
+                }
+            }
+            f32x4_t (&dS)[2][2] = dP;
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                {
+                }
+            }
+            // ---- dS through LDS (row-major [i][j]) for dQ's A operand ----
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) tbuf[(16 * ti + 4 * q4 + g) * kMmaPitch + 16 * tj + c16] = dS[ti][tj][g];
+            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
+            // ---- dV^T = dctx^T P  (rows d, columns j; k = i) ----
+            f32x4_t dVt[2][2];
+#pragma unroll
+            for (int td = 0; td < 2; td++)
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++) dVt[td][tj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            // ---- dK^T = Q^T dS  (rows k, columns j; k-dim = i) ----
+            f32x4_t dKt[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ib = 0; ib < 2; ib++) {
+                s16x4 bp[2][3], bs[2][3];
+#pragma unroll
+                for (int tj = 0; tj < 2; tj++) {
+                    const float pv[4] = {P[ib][tj][0], P[ib][tj][1], P[ib][tj][2], P[ib][tj][3]};
+                    const float sv[4] = {dS[ib][tj][0], dS[ib][tj][1], dS[ib][tj][2], dS[ib][tj][3]};
+                    split4(pv, bp[tj]);
+                    split4(sv, bs[tj]);
+                }
+#pragma unroll
+                for (int td = 0; td < 2; td++) {
+                    const int d = 16 * td + c16;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int i = 16 * ib + 4 * q4 + e;
+                        v[e] = (i < kTok && d < kEmb) ? dhr[i * kEmb + d] : 0.f;
+                    }
+                    s16x4 a[3];
+                    split4(v, a);
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++) dVt[td][tj] = mma16x3(a, bp[tj], dVt[td][tj]);
+                }
+                {
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++)
+                        v[e] = c16 < kKq ? qkv(16 * ib + 4 * q4 + e, c16, xk(16 * ib + 4 * q4 + e)) : 0.f;
+                    s16x4 a[3];
+                    split4(v, a);
+#pragma unroll
+                    for (int tj = 0; tj < 2; tj++) dKt[tj] = mma16x3(a, bs[tj], dKt[tj]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
+            // ---- dQ = dS K  (rows i, columns k; k-dim = j) ----
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            f32x4_t dQ[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int jb = 0; jb < 2; jb++) {
+                float w[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    w[e] = c16 < kKq ? qkv(16 * jb + 4 * q4 + e, kKq + c16, xk(16 * jb + 4 * q4 + e)) : 0.f;
+                s16x4 b[3];
+                split4(w, b);
+#pragma unroll
+                for (int ti = 0; ti < 2; ti++) {
+                    const float4 r4 = *reinterpret_cast<const float4*>(tbuf + (16 * ti + c16) * kMmaPitch + 16 * jb +
+                                                                       4 * q4);
+                    const float v[4] = {r4.x, r4.y, r4.z, r4.w};
+                    s16x4 a[3];
+                    split4(v, a);
+                    dQ[ti] = mma16x3(a, b, dQ[ti]);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
+            // ---- the reduction operands of this sample: G = [dq | dk | dv], dctx, x ----
+#pragma unroll
+            for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int i = 16 * ti + 4 * q4 + g;
+                    if (i < kTok && c16 < kKq) my[kMG + i * kQkv + c16] = dQ[ti][g];
+                }
+#pragma unroll
+            for (int tj = 0; tj < 2; tj++) {
+                const int j = 16 * tj + c16;
+                if (j < kTok) {
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        const int k = 4 * q4 + g;
+                        if (k < kKq) my[kMG + j * kQkv + kKq + k] = dKt[tj][g];
+                    }
+#pragma unroll
+                    for (int td = 0; td < 2; td++) {
+                        const int d0 = 16 * td + 4 * q4;
+                        if (d0 < kEmb)
+                            *reinterpret_cast<float4*>(my + kMG + j * kQkv + 2 * kKq + d0) =
+                                make_float4(dVt[td][tj][0], dVt[td][tj][1], dVt[td][tj][2], dVt[td][tj][3]);
                     }
                 }
             }
+            for (int e = lane; e < kTok * kEmb / 4; e += 64)
+                *reinterpret_cast<float4*>(my + kMD + 4 * e) = *reinterpret_cast<const float4*>(dhr + 4 * e);
         }
+        __syncthreads();
+        ef_accumulate<kMmaSample, kMG, kMD, kMX>(sm, nrow, ae, as);
     }
-    float* out = partial + (size_t)blockIdx.x * kPartLen;
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-        const int unit = threadIdx.x + u * kBwdThreads;
-        if (unit < kEFUnits) {
-            const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
-#pragma unroll
-            for (int a = 0; a < 4; a++) {
-                *reinterpret_cast<float4*>(out + kPEF + (tk * kGd + r0 + a) * kPin) =
-                    make_float4(ae[u][a][0], ae[u][a][1], ae[u][a][2], ae[u][a][3]);
-                out[kPef + tk * kGd + r0 + a] = as[u][a];
-            }
-        }
-    }
+    ef_write(partial, ae, as);
 }
 
 // sum of the partial rows: workgroup = 64 columns x 16 row classes (r mod 16);
@@ -602,11 +952,15 @@ extern "C" int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int 
     return (int)hipGetLastError();
 }
 
-extern "C" int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
-                                  float* partial, int grid, float* red, float* grad, void* stream) {
+extern "C" int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
+                                     float* partial, int grid, float* red, float* grad, int algo, void* stream) {
     if (!ws || !x || !dh || !partial || !red || !grad || B < 0 || ldx < MM_OBS_DIM || grid <= 0) return MM_E_ARG;
+    if (algo != MM_FRONT_BWD_MFMA && algo != MM_FRONT_BWD_VALU) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
+    if (algo == MM_FRONT_BWD_MFMA)
+        hipLaunchKernelGGL(k_front_bwd_mfma, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
+    else
+        hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_front_sum, dim3((kPartLen + kSumCols - 1) / kSumCols), dim3(kSumCols * kSumClasses), 0, s,
@@ -615,4 +969,9 @@ extern "C" int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int 
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_front_combine, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, grad);
     return (int)hipGetLastError();
+}
+
+extern "C" int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
+                                  float* partial, int grid, float* red, float* grad, void* stream) {
+    return mm_actor_front_bwd_ex(ws, x, ldx, B, parity, dh, partial, grid, red, grad, MM_FRONT_BWD_VALU, stream);
 }

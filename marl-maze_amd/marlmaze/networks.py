@@ -79,6 +79,9 @@ class m_Attention(nn.Module):
 
 
 _CUS = {}
+# the front-end backward's attention products: "valu" (fp32 FMA, the default) or "mfma" (bf16x3 MFMA tiles;
+# measured slower, csrc/actor_front.hip k_front_bwd_mfma)
+FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "valu")
 
 
 def _cu_count(dev):
@@ -132,9 +135,9 @@ class _FusedFront(torch.autograd.Function):
         partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
         red = torch.empty(plen, dtype=torch.float32, device=x.device)
         g = torch.empty(L.mm_actor_front_grad_len(), dtype=torch.float32, device=x.device)
-        _lib.check(L.mm_actor_front_bwd(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(ctx.parity), _lib.ptr(dh),
-                                        _lib.ptr(partial), grid, _lib.ptr(red), _lib.ptr(g), _lib.stream_ptr()),
-                   "mm_actor_front_bwd")
+        _lib.check(L.mm_actor_front_bwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(ctx.parity), _lib.ptr(dh),
+                                           _lib.ptr(partial), grid, _lib.ptr(red), _lib.ptr(g),
+                                           _lib.FRONT_BWD[FRONT_BWD_ALGO], _lib.stream_ptr()), "mm_actor_front_bwd_ex")
         n_qk, n_v = KQ_DIM * EMBEDDING_DIM, EMBEDDING_DIM * EMBEDDING_DIM
         dwq = g[0:n_qk].view(KQ_DIM, EMBEDDING_DIM)
         dwk = g[n_qk:2 * n_qk].view(KQ_DIM, EMBEDDING_DIM)

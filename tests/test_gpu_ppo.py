@@ -167,10 +167,15 @@ def test_train_runs_and_learns_something():
     assert ag.history[-1]["episodes"] > 0
 
 
+@pytest.mark.parametrize("algo", ["mfma", "valu"])
 @pytest.mark.parametrize("parity", [True, False])
-def test_fused_front_matches_torch(parity):
-    """csrc/actor_front.hip forward+backward == the module-by-module torch path."""
+def test_fused_front_matches_torch(parity, algo, monkeypatch):
+    """csrc/actor_front.hip forward+backward == the module-by-module torch path
+    (both backward algorithms: the MFMA attention products and the VALU form)."""
+    from marlmaze import networks
     from marlmaze.networks import Actor, _FusedFront, front_params
+
+    monkeypatch.setattr(networks, "FRONT_BWD_ALGO", algo)
 
     torch.manual_seed(0)
     actor = Actor([264, 264, 264], parity_mode=parity).cuda()
@@ -190,6 +195,44 @@ def test_fused_front_matches_torch(parity):
     g = torch.autograd.grad(h, params, dh)
     for a, b in zip(g, gref):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-3 * b.abs().max().item())
+
+
+@pytest.mark.parametrize("parity", [True, False])
+def test_front_backward_mfma_vs_fp64(parity, monkeypatch):
+    """The front-end's parameter gradients against an fp64 evaluation of the
+    same modules: the MFMA backward (bf16x3 products, fp32-class) is as close to
+    fp64 as the VALU fp32 backward -- within twice its error, and within 1e-5
+    of each tensor's max|g| (sums over 20,000 samples)."""
+    from marlmaze import networks
+    from marlmaze.networks import Actor, _FusedFront, front_params
+
+    torch.manual_seed(1)
+    actor = Actor([264, 264, 264], parity_mode=parity).cuda()
+    with torch.no_grad():
+        for p in actor.parameters():
+            p.mul_(3.0)
+    B = 20000
+    x = torch.randn(B, 65, device="cuda")
+    if parity:  # the facing one-hot the env writes (the actor reads only obs[0:4], Q1)
+        x[:, :4] = torch.nn.functional.one_hot(torch.randint(0, 4, (B,), device="cuda"), 4).float()
+    dh = torch.randn(B, 460, device="cuda") / B
+    params = front_params(actor.projection, actor.attention)
+    a64 = Actor([264, 264, 264], parity_mode=parity).double()
+    a64.load_state_dict({k: v.detach().cpu().double() for k, v in actor.state_dict().items()})
+    p64 = front_params(a64.projection, a64.attention)
+    h64 = a64.attention(a64.projection(x.cpu().double()))
+    g64 = torch.autograd.grad(h64, p64, dh.cpu().double())
+    errs = {}
+    for algo in ("mfma", "valu"):
+        monkeypatch.setattr(networks, "FRONT_BWD_ALGO", algo)
+        h = _FusedFront.apply(x, parity, *params)
+        g = torch.autograd.grad(h, params, dh)
+        errs[algo] = [((a.double().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+                      for a, b in zip(g, g64)]
+    worst = max(range(len(g64)), key=lambda k: errs["mfma"][k])
+    print(f"front bwd vs fp64 (parity={parity}): mfma max {errs['mfma'][worst]:.2e}, valu {errs['valu'][worst]:.2e}")
+    for k in range(len(g64)):
+        assert errs["mfma"][k] <= max(2 * errs["valu"][k], 1e-5), (k, errs["mfma"][k], errs["valu"][k])
 
 
 def test_checkpoint_round_trip_reference_format(tmp_path, golden):
