@@ -4,7 +4,7 @@
 set -e
 mkdir -p tools/_var gpurun_out
 SRC=marl-maze_amd/csrc
-for v in BASE NO_EPI NO_DMA NO_ALOAD NO_DMA_NO_ALOAD; do
+for v in BASE NO_DMA NO_ALOAD NO_DMA_NO_ALOAD; do
   defs=""
   case $v in
     NO_EPI) defs="-DX3_NO_EPI";;
@@ -12,7 +12,7 @@ for v in BASE NO_EPI NO_DMA NO_ALOAD NO_DMA_NO_ALOAD; do
     NO_ALOAD) defs="-DX3_NO_ALOAD";;
     NO_DMA_NO_ALOAD) defs="-DX3_NO_DMA -DX3_NO_ALOAD";;
   esac
-  if [ ! -f tools/_var/x3_$v.so ]; then
+  if true; then
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -ffp-contract=off $defs -I include -I $SRC \
       -o tools/_var/x3_$v.so $SRC/*.hip
   fi
