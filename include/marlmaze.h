@@ -266,6 +266,14 @@ int mm_gemm_tp_pack(int prec, const float* X, int R, int C, int ld, int trans, u
 int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
                const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out, float* colsum, float cscale,
                float* c, int ldc, void* stream);
+/* mm_gemm_nt_algo: which kernel mm_gemm_nt / mm_x3_nt_f32a use (process-wide; returns the previous
+ * setting).  MM_GEMM_AUTO: the B-resident kernel (a column block of B kept in LDS for the whole launch,
+ * independent waves) where the shape fits it (M >= 16384, B block of >= 4 tiles), else the streaming
+ * kernel; MM_GEMM_STREAM: always the streaming kernel (B through LDS one k-step at a time).  Initial
+ * value: MM_GEMM_STREAM if the environment sets MARLMAZE_GEMM_BRES=0, else MM_GEMM_AUTO. */
+#define MM_GEMM_AUTO 0
+#define MM_GEMM_STREAM 1
+int mm_gemm_nt_algo(int algo);
 long mm_gemm_wgrad_ws_len(int M, int N, int K);
 int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
                   float cscale, float* ws, float* dw, void* stream);

@@ -44,6 +44,7 @@
 // along a run), and the row slices' partials are summed in a fixed order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -456,6 +457,19 @@ __device__ __forceinline__ void epilogue_tp(const f32x4 (&acc)[NT], float* slice
 // DMA issues spread over the MFMA stream.  One barrier per k-step; four waves
 // per SIMD hide the LDS latency of the B fragment reads.  Persistent over
 // 256-row units.
+#ifdef X3_STAMPS  // diagnostic builds only (tools/x3_stamps.sh): per-wave phase clocks of k_x3nt
+__device__ unsigned long long g_x3_stamps[256 * 16 * kWaves * 8];
+#define X3_STAMP(it, slot, val)                                                                       \
+    do {                                                                                              \
+        if (lane == 0 && blockIdx.x < 256 && (it) < 16)                                               \
+            g_x3_stamps[((blockIdx.x * 16 + (it)) * kWaves + wave) * 8 + (slot)] = (val);             \
+    } while (0)
+#else
+#define X3_STAMP(it, slot, val) \
+    do {                        \
+    } while (0)
+#endif
+
 template <int NT, int P, class AS, class AT, int EM>
 __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int lda, float ascale,
                                                    const uint16_t* __restrict__ B, int M, int N, int K, int nks,
@@ -478,6 +492,10 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         const int rb = (slot / ncb) * 8 + xcd, cb = slot % ncb;
         if (rb >= nrb) continue;  // workgroup-uniform
         const int rt = rb * kWaves + wave;  // this wave's row tile
+        const int it = (u - (int)blockIdx.x) / (int)gridDim.x;
+        (void)it;
+        X3_STAMP(it, 0, __builtin_amdgcn_s_memtime());
+        X3_STAMP(it, 4, __builtin_amdgcn_s_memrealtime());
         AS as;
         as.init(A, rt, nks, M, lda, K, ascale);
         const uint16_t* Bg = B + (size_t)cb * NT * nks * Prec<P>::kBlk;
@@ -496,6 +514,7 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         for (int i = wave; i < C::kPiecesB; i += kWaves) dma_b<P>(Bg, nks, 0, i, sB0 + i * 512, lane);
         as.load(0, r0, lane);
         __syncthreads();
+        X3_STAMP(it, 1, __builtin_amdgcn_s_memtime());
         // k-steps in pairs so the two stage buffers are compile-time distinct
         // (no wait of a B fragment read on the other buffer's DMA)
         int ks = 0;
@@ -504,6 +523,7 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
             k_step<NT, P>(acc, as, r1, r0, Bg, nks, ks + 1, sB1, sB0, wave, lane);
         }
         if (ks < nks) k_step<NT, P>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
+        X3_STAMP(it, 2, __builtin_amdgcn_s_memtime());
 
         // ---- epilogue (after the last k-step's barrier both stage buffers are free) ----
         if constexpr (EM == EM_TP)
@@ -515,6 +535,8 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+        X3_STAMP(it, 3, __builtin_amdgcn_s_memtime());
+        X3_STAMP(it, 5, __builtin_amdgcn_s_memrealtime());
     }
 }
 
@@ -938,10 +960,378 @@ __global__ __launch_bounds__(256) void k_wg_reduce(const float* __restrict__ ws,
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_bres: C[M, N] = A[M, K] . B[N, K]^T with a column block of B RESIDENT in
+// LDS for the whole launch (the forward and input-gradient GEMMs of the actor
+// and critic, K <= 288 for x3).  Why (tools/x3_stamps.py on k_x3nt, 264 x 264,
+// M = 419,430): k_x3nt streams B through LDS one k-step at a time, so its 16
+// waves meet at a barrier every k-step and split A, read B and issue MFMAs in
+// lock-step: 12.2k cycles per k-step against 6.5k of MFMA work, plus 15k of
+// prologue and 21k of epilogue per 256-row unit that no other wave overlaps.
+// Here each workgroup loads its block of B once (LDS-DMA), and after one
+// barrier its waves run independently: a wave owns 32 rows (two row tiles)
+// x <= CT column tiles at a time, loads and splits its own A (fp32, one
+// k-step ahead), reads B fragments from LDS (each feeds both row tiles) and
+// writes its outputs -- one wave's loads and stores overlap the others'
+// MFMAs, and nothing waits for the slowest wave.
+//
+// Column blocks: B of a tile over the whole K is planes x (32-wide steps x 1
+// KiB + a final 16-wide step x 512 B when K % 32 is 1..16, on the 16x16x16
+// MFMA); the block is as many tiles as fit 160 KiB (x3, K = 264: 6 tiles ->
+// 17 = 6 + 6 + 5; f16: all 17).  Workgroups of one XCD split over the blocks
+// in proportion to their tiles, and the XCD takes every 8th 32-row unit, so
+// the blocks re-reading a unit's A rows do it through the same L2.  Waves
+// whose block is wider than CT take the sub-blocks of a unit in turn (A again
+// from L1 / L2).
+struct BresPlan {
+    int xcds;   // XCDs the grid spreads over (8, or 1)
+    int nblk;   // column blocks
+    int ctb;    // column tiles per block (the last may have fewer)
+    int tiles;  // column tiles of the output
+    int nfull;  // 32-wide k-steps
+    int half;   // 1: a final 16-wide k-step
+    int first[9];  // per XCD: block b's workgroups are first[b] .. first[b + 1] - 1
+};
+constexpr int kBresMaxBlk = 8;
+
+// A through a buffer resource: a load whose offset is past the buffer's end returns zeros, so the
+// columns past K cost one select of the offset -- no branch, and no wait on the loaded value (a select
+// on the value, or two load forms merged at a branch, made the compiler wait for each k-step's loads
+// at the end of the step that issued them: no prefetch at all)
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
+constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past every buffer (num_records < 2^31)
+
+struct BresA {
+    __amdgpu_buffer_rsrc_t rsrc;  // A: base, num_records = M lda 4 bytes
+    uint32_t roff[2];             // this lane's row of row tile r (r < RT), + 4 kq bytes
+};
+
+// A for one 32-wide k-step: row tile r's lane row, columns k = 32 ks + 4 (l >> 4) .. +3 and +16 .. +19;
+// zeros at columns >= K
+template <int RT, int VW>
+__device__ __forceinline__ void bres_load(const BresA& as, int ks, int K, int kq, float4 (&raw)[RT][2]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int kk = 32 * ks + kq + 16 * h;
+#pragma unroll
+        for (int r = 0; r < RT; r++) {
+            const uint32_t o = as.roff[r] + 4u * (32 * ks + 16 * h);
+            if constexpr (VW == 4) {
+                const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(as.rsrc, kk < K ? o : kBufOOB, 0, 0);
+                raw[r][h] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                                        __uint_as_float(v.w));
+            } else {
+                const u32x2v a = __builtin_amdgcn_raw_buffer_load_b64(as.rsrc, kk < K ? o : kBufOOB, 0, 0);
+                const u32x2v b = __builtin_amdgcn_raw_buffer_load_b64(as.rsrc, kk + 2 < K ? o + 8 : kBufOOB, 0, 0);
+                raw[r][h] = make_float4(__uint_as_float(a.x), __uint_as_float(a.y), __uint_as_float(b.x),
+                                        __uint_as_float(b.y));
+            }
+        }
+    }
+}
+
+// 8 fp32 -> the precision's A fragment planes (P_X3: exact three-way split; P_F16: x * s rounded)
+template <int P>
+__device__ __forceinline__ void bres_frag(const float4 (&r)[2], float s, bf16x8 (&a)[3]) {
+#ifdef BRES_NO_SPLIT  // diagnostic builds only: the raw bits as fragments (no split VALU; outputs wrong)
+    a[0] = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(r[0].x), __float_as_uint(r[0].y),
+                                                 __float_as_uint(r[1].x), __float_as_uint(r[1].y)));
+    a[1] = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(r[0].z), __float_as_uint(r[0].w),
+                                                 __float_as_uint(r[1].z), __float_as_uint(r[1].w)));
+    a[2] = a[0];
+    return;
+#endif
+    if constexpr (P == P_X3) {
+        uint32_t h[4], m[4], l[4];
+        split2(r[0].x, r[0].y, h[0], m[0], l[0]);
+        split2(r[0].z, r[0].w, h[1], m[1], l[1]);
+        split2(r[1].x, r[1].y, h[2], m[2], l[2]);
+        split2(r[1].z, r[1].w, h[3], m[3], l[3]);
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+        a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
+        a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    } else {
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(f16x2_rn(r[0].x * s, r[0].y * s), f16x2_rn(r[0].z * s, r[0].w * s),
+                                                     f16x2_rn(r[1].x * s, r[1].y * s), f16x2_rn(r[1].z * s, r[1].w * s)));
+    }
+}
+
+// the final 16-wide step: the 4 values k = 4 (l >> 4) .. +3 (the j < 4 half of a TP piece)
+template <int P>
+__device__ __forceinline__ void bres_frag16(const float4& r, float s, uint2 (&a)[3]) {
+    if constexpr (P == P_X3) {
+        uint32_t h[2], m[2], l[2];
+        split2(r.x, r.y, h[0], m[0], l[0]);
+        split2(r.z, r.w, h[1], m[1], l[1]);
+        a[0] = make_uint2(h[0], h[1]);
+        a[1] = make_uint2(m[0], m[1]);
+        a[2] = make_uint2(l[0], l[1]);
+    } else {
+        a[0] = make_uint2(f16x2_rn(r.x * s, r.y * s), f16x2_rn(r.z * s, r.w * s));
+    }
+}
+
+template <int P>
+__device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x4 acc) {
+    typedef __attribute__((ext_vector_type(4))) short s4;
+    if constexpr (P == P_X3) {
+#define MM_B16(x) __builtin_bit_cast(s4, x)
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[2]), MM_B16(b[0]), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[0]), MM_B16(b[2]), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[1]), MM_B16(b[1]), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[1]), MM_B16(b[0]), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[0]), MM_B16(b[1]), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[0]), MM_B16(b[0]), acc, 0, 0, 0);
+#undef MM_B16
+    } else {
+        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+        acc = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a[0]), __builtin_bit_cast(h4, b[0]), acc, 0,
+                                                     0, 0);
+    }
+    return acc;
+}
+
+// Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even).  ReLU bits:
+// bit 4 c + g of the tile-local word = bit 4 (tg0 + c) + g of the row tile's mask, i.e. local byte m is
+// global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD) whole bytes of its own tiles.
+template <int P, int CT, int EM, bool FULL>
+__device__ __forceinline__ void bres_epi(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
+                                         const Epi& ep, const float* sb, int lane) {
+    constexpr int NW = (4 * CT + 31) / 32;  // local mask words
+    int rq = 4 * (lane >> 4);
+    asm volatile("" : "+v"(rq));  // row addresses formed here, not hoisted over the main loop and held
+    uint32_t lbits[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) lbits[w] = 0u;
+    if (EM == EM_BWD) {
+        const uint8_t* mi =
+            reinterpret_cast<const uint8_t*>(ep.mbits_in + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
+#pragma unroll
+        for (int m = 0; m < (CT + 1) / 2; m++)
+            if (2 * m < ctn) lbits[m >> 2] |= (uint32_t)mi[m] << (8 * (m & 3));
+    }
+    const float* sbl = sb + (lane & 15);
+    // FULL: every row and column of the tile exists -- no per-element checks, one row pointer per g and
+    // the columns at immediate offsets
+    float* crow = ep.c + (size_t)(16 * rt + rq) * ep.ldc + 16 * tg0 + (lane & 15);
+#pragma unroll
+    for (int c = 0; c < CT; c++) {
+        if (c >= ctn || 16 * (tg0 + c) >= N) continue;  // wave-uniform (continue: the loop stays unrolled)
+        const int col = 16 * (tg0 + c) + (lane & 15);
+        const float bv = (EM != EM_BWD && ep.bias) ? sbl[16 * c] : 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int row = 16 * rt + rq + g, bit = 4 * c + g;
+            float x = acc[c][g];
+            if (P == P_F16) x *= ep.cscale;
+            if (EM == EM_BWD) {
+                if (!((lbits[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
+            } else {
+                x += bv;
+                if (ep.relu) x = fmaxf(x, 0.f);
+            }
+            if (FULL && 16 * (tg0 + c) + 16 <= N) {  // the whole tile inside N (wave-uniform)
+                if (EM == EM_FWD) lbits[bit >> 5] |= (x > 0.f ? 1u : 0u) << (bit & 31);
+#ifdef BRES_NO_STORE  // diagnostic builds only
+                if (x == 1234.5f)
+#endif
+                crow[(size_t)g * ep.ldc + 16 * c] = x;
+            } else {
+                if (EM == EM_FWD && x > 0.f && col < N && row < M) lbits[bit >> 5] |= 1u << (bit & 31);
+                if (row < M && col < N) ep.c[(size_t)row * ep.ldc + col] = x;
+            }
+        }
+        if (EM == EM_BWD && ep.colsum) {
+            float cs = 0.f;
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int row = 16 * rt + rq + g;
+                const float v = P == P_F16 ? acc[c][g] * ep.cscale : acc[c][g];
+                const int bit = 4 * c + g;
+                if ((FULL || row < M) && ((lbits[bit >> 5] >> (bit & 31)) & 1u)) cs += v;
+            }
+            cs += __shfl_xor(cs, 16);
+            cs += __shfl_xor(cs, 32);
+            if (lane < 16 && col < N && (FULL || 16 * rt < M)) ep.colsum[(size_t)rt * N + col] = cs;
+        }
+    }
+    if (EM == EM_FWD) {
+        uint8_t* mb = reinterpret_cast<uint8_t*>(ep.mbits_out + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
+#pragma unroll
+        for (int m = 0; m < (CT + 1) / 2; m++)
+            if (2 * m < ctn) mb[m] = (uint8_t)(lbits[m >> 2] >> (8 * (m & 3)));
+    }
+}
+
+template <int P, int CT, int EM>
+__device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
+                                              const Epi& ep, const float* sb, int lane) {
+    if (16 * rt + 16 <= M)  // wave-uniform; columns past N checked per tile
+        bres_epi<P, CT, EM, true>(acc, rt, tg0, ctn, M, N, ep, sb, lane);
+    else
+        bres_epi<P, CT, EM, false>(acc, rt, tg0, ctn, M, N, ep, sb, lane);
+}
+
+// one 32-wide k-step: cur -> fragments, step ks + 1 -> nxt (past the last step: offsets past K, zeros),
+// the CT column tiles' MFMAs for both row tiles (each B fragment read feeds both)
+template <int P, int CT, int RT, int VW>
+__device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&cur)[RT][2], float4 (&nxt)[RT][2],
+                                          const BresA& as, int ks, int K, int kq, int ctb, int c0, int ctn,
+                                          float ascale, const uint16_t* sF, int lane) {
+    constexpr int np = Prec<P>::kPlanes;
+    bf16x8 a[RT][3];
+#pragma unroll
+    for (int r = 0; r < RT; r++) bres_frag<P>(cur[r], ascale, a[r]);
+    bres_load<RT, VW>(as, ks + 1, K, kq, nxt);
+    int boff = ((ks * ctb + c0) * np) * 64 + lane;  // bf16x8 units
+    asm volatile("" : "+v"(boff));                  // one base per step (not 18 hoisted addresses)
+    const bf16x8* bp = reinterpret_cast<const bf16x8*>(sF) + boff;
+#pragma unroll
+    for (int c = 0; c < CT; c++) {
+        if (c < ctn) {  // wave-uniform (a guard, not a break: the loop stays fully unrolled, acc in registers)
+            bf16x8 bb[3];
+#pragma unroll
+            for (int q = 0; q < np; q++) bb[q] = bp[(c * np + q) * 64];
+#pragma unroll
+            for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb, acc[r][c]);
+        }
+    }
+}
+
+template <int P, int CT, int RT, int EM, int VW>
+__global__ __launch_bounds__(kThreads) void k_bres(const float* __restrict__ A, int lda, float ascale,
+                                                   const uint16_t* __restrict__ B, int M, int N, int K, int nks,
+                                                   BresPlan pl, Epi ep) {
+    static_assert(EM == EM_F32 || EM == EM_FWD || EM == EM_BWD, "fp32 outputs");
+    constexpr int np = Prec<P>::kPlanes;
+    extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int X = pl.xcds, x = (int)blockIdx.x % X, wi = (int)blockIdx.x / X;
+    X3_STAMP(0, 0, __builtin_amdgcn_s_memtime());
+    X3_STAMP(0, 4, __builtin_amdgcn_s_memrealtime());
+    if (wi >= pl.first[pl.nblk]) return;  // a surplus workgroup: uniform, before any barrier
+    int b = 0;
+    while (b + 1 < pl.nblk && wi >= pl.first[b + 1]) b++;
+    const int t0 = b * pl.ctb, ctb = min(pl.ctb, pl.tiles - t0);
+    const int nfull = pl.nfull, half = pl.half;
+    uint16_t* sF = smem;                               // [nfull][ctb][np][512]: a step's pieces at immediate offsets
+    uint16_t* sT = smem + (size_t)ctb * nfull * np * 512;  // [ctb][np][256]: the 16-wide step
+    float* sbias = reinterpret_cast<float*>(sT + ctb * np * 256 * half);
+
+    // ---- the block of B -> LDS, once ----
+    const int nF = ctb * nfull * np;
+    for (int p = wave; p < nF; p += kWaves) {
+        const int q = p % np, cks = p / np, c = cks % ctb, ks = cks / ctb;
+        const uint4* src =
+            reinterpret_cast<const uint4*>(B + ((size_t)(t0 + c) * nks + ks) * Prec<P>::kBlk + q * 512);
+        __builtin_amdgcn_global_load_lds(src + lane, sF + (size_t)p * 512, 16, 0, 0);
+    }
+    if (half) {
+        for (int p = wave; p < ctb * np; p += kWaves) {
+            const int q = p % np, c = p / np;
+            const uint2* src =
+                reinterpret_cast<const uint2*>(B + ((size_t)(t0 + c) * nks + nfull) * Prec<P>::kBlk + q * 512);
+            reinterpret_cast<uint2*>(sT + p * 256)[lane] = src[2 * lane];
+        }
+    }
+    if (EM != EM_BWD && ep.bias)
+        for (int t = threadIdx.x; t < ctb * 16; t += kThreads) {
+            const int col = 16 * t0 + t;
+            sbias[t] = col < N ? ep.bias[col] : 0.f;
+        }
+    __syncthreads();  // vmcnt(0) + barrier: every wave's DMA pieces and writes landed
+    X3_STAMP(0, 1, __builtin_amdgcn_s_memtime());
+
+    // ---- independent waves ----
+    // the workgroup takes groups of 16 consecutive 32-row units (512 rows, one per wave): groups
+    // x + X (wb + nW t) for t = 0, 1, ...  -- each CU's loads and stores stay inside one ~0.5 MB stretch
+    // of A and C at a time (scattering a workgroup's waves over the matrix measured ~2x slower)
+    const int nu = (M + 16 * RT - 1) / (16 * RT);
+    const int nW = pl.first[b + 1] - pl.first[b], wb = wi - pl.first[b];
+    const int nsb = (ctb + CT - 1) / CT;
+    const int kq = 4 * (lane >> 4);
+    // gfx9 buffer resource word 3 0x00020000: 32-bit data format, raw (stride 0) addressing
+    const __amdgpu_buffer_rsrc_t arsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((size_t)M * lda * 4), 0x00020000);
+    for (int t = 0;; t++) {
+        const int u = (x + X * (wb + nW * t)) * kWaves + wave;
+        if (u >= nu) break;
+        BresA as;
+        as.rsrc = arsrc;
+#pragma unroll
+        for (int r = 0; r < RT; r++) {
+#ifdef BRES_ROW0  // diagnostic builds only: every unit reads the first 32 rows (A L2-resident; outputs wrong)
+            const int row = min(16 * r + (lane & 15), M - 1);
+#else
+            const int row = min(16 * (RT * u + r) + (lane & 15), M - 1);  // rows past M: computed, not stored
+#endif
+            as.roff[r] = 4u * ((uint32_t)row * (uint32_t)lda + (uint32_t)kq);
+        }
+        for (int s = 0; s < nsb; s++) {
+            const int c0 = s * CT, ctn = min(CT, ctb - c0);
+            f32x4 acc[RT][CT];
+#pragma unroll
+            for (int r = 0; r < RT; r++)
+#pragma unroll
+                for (int c = 0; c < CT; c++) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // two A buffers, steps in pairs: step ks splits cur and loads step ks + 1 into nxt, so the
+            // loads stay in flight over a whole step (one buffer made the compiler copy at the loop end,
+            // waiting for the loads it had just issued)
+            float4 rawA[RT][2], rawB[RT][2];
+            bres_load<RT, VW>(as, 0, K, kq, rawA);
+            int ks = 0;
+            for (; ks + 2 <= nfull; ks += 2) {
+                bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                bres_step<P, CT, RT, VW>(acc, rawB, rawA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+            }
+            const bool odd = ks < nfull;
+            if (odd) bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+            if (half) {
+                uint2 a4[RT][3];
+#pragma unroll
+                for (int r = 0; r < RT; r++) bres_frag16<P>(odd ? rawB[r][0] : rawA[r][0], ascale, a4[r]);
+                const uint2* bp = reinterpret_cast<const uint2*>(sT) + (size_t)(c0 * np) * 64 + lane;
+#pragma unroll
+                for (int c = 0; c < CT; c++) {
+                    if (c < ctn) {
+                        uint2 bb[3];
+#pragma unroll
+                        for (int q = 0; q < np; q++) bb[q] = bp[(c * np + q) * 64];
+#pragma unroll
+                        for (int r = 0; r < RT; r++) acc[r][c] = mma16<P>(a4[r], bb, acc[r][c]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < RT; r++)
+                bres_epilogue<P, CT, EM>(acc[r], RT * u + r, t0 + c0, ctn, M, N, ep, sbias + 16 * c0, lane);
+        }
+        X3_STAMP(1 + t, 2, __builtin_amdgcn_s_memtime());  // end of unit t
+    }
+    X3_STAMP(0, 3, __builtin_amdgcn_s_memtime());
+    X3_STAMP(0, 5, __builtin_amdgcn_s_memrealtime());
+}
+
 }  // namespace x3
 }  // namespace mm
 
 using namespace mm::x3;
+
+#ifdef X3_STAMPS
+extern "C" int mm_x3_stamps_read(unsigned long long* out, long n) {
+    const long cap = (long)(sizeof(g_x3_stamps) / sizeof(g_x3_stamps[0]));
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_stamps), (n < cap ? n : cap) * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int mm_x3_stamps_clear() {
+    static unsigned long long zero[256 * 16 * kWaves * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_x3_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess
+               ? 0 : -1;
+}
+#endif
 
 extern "C" long mm_x3_tp_len(int R, int C) { return (long)(rup(R, kRowPad) / 16) * (rup(C, 32) / 32) * kBlk; }
 
@@ -1044,6 +1434,109 @@ static int dispatch_nt_u(const float* a, int lda, float ascale, const uint16_t* 
     return MM_E_ARG;
 }
 
+// ---- k_bres dispatch ----
+static int g_gemm_algo = -1;  // MM_GEMM_*; -1: not read from the environment yet
+static bool bres_enabled() {
+    if (g_gemm_algo < 0) {
+        const char* e = getenv("MARLMAZE_GEMM_BRES");
+        g_gemm_algo = (e && e[0] == '0') ? MM_GEMM_STREAM : MM_GEMM_AUTO;
+    }
+    return g_gemm_algo == MM_GEMM_AUTO;
+}
+
+extern "C" int mm_gemm_nt_algo(int algo) {
+    bres_enabled();
+    const int prev = g_gemm_algo;
+    if (algo == MM_GEMM_AUTO || algo == MM_GEMM_STREAM) g_gemm_algo = algo;
+    return prev;
+}
+
+constexpr int kBresMinRows = 16384;
+// wave units: C_NARROW two row tiles x 6 column tiles (acc 48 registers; each B fragment read feeds two
+// tiles) -- x3, and f16 up to 6 tiles; C_WIDE (f16) one row tile x up to 17 column tiles (acc 68: the
+// whole 264-wide output per wave, A read once)
+enum { C_NARROW = 0, C_WIDE = 1 };
+template <int C> struct BresCfg { static constexpr int CT = C == C_NARROW ? 6 : 17, RT = C == C_NARROW ? 2 : 1; };
+
+// The column blocks and the per-XCD workgroup split (see k_bres); false: the shape does not fit.
+static bool bres_plan(int prec, int M, int N, int K, int lda, bool bits, BresPlan& pl, int& cfg) {
+    if (M < kBresMinRows || (size_t)M * lda * 4 >= ((size_t)1 << 31)) return false;  // A through a buffer resource
+    const int np = prec == MM_PREC_X3 ? 3 : 1;
+    const int tiles = (N + 15) / 16;
+    const int nks = rup(K, 32) / 32, rem = K % 32;
+    pl.half = rem != 0 && rem <= 16;
+    pl.nfull = nks - pl.half;
+    const long tile_bytes = (long)np * (pl.nfull * 1024L + pl.half * 512L) + 64;  // + the bias columns
+    int cmax = (int)((160L * 1024) / tile_bytes);
+    if (cmax >= tiles) cmax = tiles;
+    else if (bits) cmax &= ~1;  // blocks start at even tiles: whole mask bytes per block
+    if (cmax < 1 || pl.nfull < 1) return false;
+    int nblk = (tiles + cmax - 1) / cmax;
+    int ctb = (tiles + nblk - 1) / nblk;
+    if (bits && nblk > 1 && (ctb & 1)) ctb++;
+    if (ctb > cmax) return false;
+    nblk = (tiles + ctb - 1) / ctb;
+    if (nblk > 1 && ctb < 4) return false;  // A re-read per block: x3 at K = 460 (3 tiles) measured slower
+    if (nblk > kBresMaxBlk) return false;
+    cfg = (prec == MM_PREC_F16 && ctb > BresCfg<C_NARROW>::CT) ? C_WIDE : C_NARROW;
+    pl.nblk = nblk;
+    pl.ctb = ctb;
+    pl.tiles = tiles;
+    const int G = persistent_grid();
+    pl.xcds = G % 8 == 0 ? 8 : 1;
+    const int per = G / pl.xcds;
+    if (per < nblk) return false;
+    // workgroups per block in proportion to its tiles: greedy on the largest tiles-per-workgroup
+    int w[kBresMaxBlk];
+    for (int bk = 0; bk < nblk; bk++) w[bk] = 1;
+    for (int left = per - nblk; left > 0; left--) {
+        int best = 0;
+        for (int bk = 1; bk < nblk; bk++) {
+            const int tb = std::min(ctb, tiles - bk * ctb), tbest = std::min(ctb, tiles - best * ctb);
+            if ((long)tb * w[best] > (long)tbest * w[bk]) best = bk;
+        }
+        w[best]++;
+    }
+    pl.first[0] = 0;
+    for (int bk = 0; bk < nblk; bk++) pl.first[bk + 1] = pl.first[bk] + w[bk];
+    for (int bk = nblk + 1; bk <= kBresMaxBlk; bk++) pl.first[bk] = pl.first[nblk];
+    return true;
+}
+
+template <int P, int C, int EM, int VW>
+static int launch_bres(const float* a, int lda, float ascale, const uint16_t* b, int M, int N, int K,
+                       const BresPlan& pl, const Epi& ep, hipStream_t s) {
+    constexpr int CT = BresCfg<C>::CT, RT = BresCfg<C>::RT;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k_bres<P, CT, RT, EM, VW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return MM_E_ARG;
+        attr = true;
+    }
+    constexpr int np = Prec<P>::kPlanes;
+    const size_t lds = (size_t)pl.ctb * np * (pl.nfull * 1024 + pl.half * 512) + (size_t)pl.ctb * 16 * 4;
+    hipLaunchKernelGGL((k_bres<P, CT, RT, EM, VW>), dim3(persistent_grid()), dim3(kThreads), lds, s, a, lda, ascale, b,
+                       M, N, K, rup(K, 32) / 32, pl, ep);
+    return (int)hipGetLastError();
+}
+
+template <int P, int C, int VW>
+static int dispatch_bres_c(const float* a, int lda, float ascale, const uint16_t* b, int M, int N, int K,
+                           const BresPlan& pl, const Epi& ep, hipStream_t s) {
+    if (ep.mbits_out) return launch_bres<P, C, EM_FWD, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+    if (ep.mbits_in) return launch_bres<P, C, EM_BWD, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+    return launch_bres<P, C, EM_F32, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+}
+
+template <int P, int VW>
+static int dispatch_bres(const float* a, int lda, float ascale, const uint16_t* b, int M, int N, int K,
+                         const BresPlan& pl, int cfg, const Epi& ep, hipStream_t s) {
+    if constexpr (P == P_F16)
+        if (cfg == C_WIDE) return dispatch_bres_c<P, C_WIDE, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+    return dispatch_bres_c<P, C_NARROW, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+}
+
 static int check_common(const uint16_t* b_tp, int M, int N, int K, const float* mask, int ldm, float* c, int ldc,
                         uint16_t* c_tp) {
     if (!b_tp || M < 0 || N <= 0 || K <= 0 || (!c && !c_tp)) return MM_E_ARG;
@@ -1082,6 +1575,15 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
     if (M == 0) return 0;
     Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale};
     hipStream_t s = (hipStream_t)stream;
+    // the B-resident kernel where it measured faster (tools/bench_gemm_ab.py): 16-byte rows, and for
+    // f16 not the input-gradient form (its 17-tile epilogue spills: at par with the streaming kernel)
+    BresPlan pl;
+    int cfg = C_NARROW;
+    if (!mask && !c_tp && v4 && !(prec == MM_PREC_F16 && mbits_in) && bres_enabled() &&
+        bres_plan(prec, M, N, K, lda, mbits_in || mbits_out, pl, cfg)) {
+        if (prec == MM_PREC_X3) return dispatch_bres<P_X3, 4>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s);
+        return dispatch_bres<P_F16, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s);
+    }
     if (prec == MM_PREC_X3)
         return v4 ? dispatch_nt<P_X3, ASrcF32>(a, lda, 1.f, b_tp, M, N, K, ep, s)
                   : dispatch_nt_u<P_X3>(a, lda, 1.f, b_tp, M, N, K, ep, s);

@@ -39,11 +39,12 @@ EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd", "mm_actor_front_bwd_ex",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
-           "mm_sum_leading", "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_wgrad_ws_len",
+           "mm_sum_leading", "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
            "mm_gemm_wgrad")
 
 PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
+GEMM_ALGO = {"auto": 0, "stream": 1}  # MM_GEMM_*
 
 
 class EnvDesc(ctypes.Structure):
@@ -124,6 +125,8 @@ def lib():
         L.mm_gemm_tp_pack.restype = i32
         L.mm_gemm_nt.argtypes = [i32, P, i32, f32, P, i32, i32, i32, P, i32, P, P, P, f32, P, i32, P]
         L.mm_gemm_nt.restype = i32
+        L.mm_gemm_nt_algo.argtypes = [i32]
+        L.mm_gemm_nt_algo.restype = i32
         L.mm_gemm_wgrad_ws_len.argtypes = [i32, i32, i32]
         L.mm_gemm_wgrad_ws_len.restype = ctypes.c_long
         L.mm_gemm_wgrad.argtypes = [i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P, P]

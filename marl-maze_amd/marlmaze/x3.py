@@ -54,6 +54,13 @@ def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None
     return out
 
 
+def set_algo(name):
+    """The kernel gemm() runs (mm_gemm_nt_algo, process-wide): "auto" = B resident in LDS where the
+    shape fits, "stream" = B streamed per k-step.  Returns the previous setting's name."""
+    prev = _lib.lib().mm_gemm_nt_algo(_lib.GEMM_ALGO[name])
+    return {v: k for k, v in _lib.GEMM_ALGO.items()}[prev]
+
+
 def wgrad(dy, x, prec="x3", dscale=1.0, out=None):
     """dW [N, K] = dY^T X summed over the M rows (mm_gemm_wgrad), dY [M, N] and
     X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two)."""

@@ -59,17 +59,29 @@ def test_wgrad_strided_and_empty():
     assert torch.equal(z, torch.zeros(6, 264, device="cuda"))
 
 
+@pytest.fixture(params=["auto", "stream"])
+def algo(request):
+    """Both forward kernels: "auto" = B resident in LDS (k_bres) where the shape fits, "stream" = k_x3nt."""
+    prev = x3.set_algo(request.param)
+    yield request.param
+    x3.set_algo(prev)
+
+
 @pytest.mark.parametrize("prec", ["x3", "f16"])
 @pytest.mark.parametrize("M,N,K", [(40000, 264, 460), (40000, 264, 264), (40000, 6, 264), (40000, 64, 130),
-                                   (40000, 1, 64), (777, 64, 64)])
-def test_gemm_forward_and_input_gradient(prec, M, N, K):
+                                   (40000, 1, 64), (777, 64, 64), (40000, 460, 264), (16411, 264, 264),
+                                   (20000, 96, 52)])
+def test_gemm_forward_and_input_gradient(prec, M, N, K, algo):
     """Forward (bias + ReLU + bit mask) and the input-gradient form (bits of the
-    layer below, per-tile column sums) in both precisions, 16- and 8-byte rows."""
+    layer below, per-tile column sums) in both precisions, 16- and 8-byte rows,
+    both kernels; ragged M (16,411: a partial last row tile and 32-row unit), K
+    with a 16-wide final step (264, 460, 130) or a partial 32-wide one (52); N = 460: no
+    bit masks (N <= 272), the plain input-gradient form."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g)
     w = torch.randn(N, K, device="cuda", generator=g) * 0.1
     b = torch.randn(N, device="cuda", generator=g)
-    bits = x3.mbits(M, "cuda")
+    bits = x3.mbits(M, "cuda") if N <= 272 else None
     y = x3.gemm(a, x3.pack(w, prec=prec), bias=b, relu=True, mbits_out=bits)
     pre = a.double() @ w.double().t() + b.double()
     scale = a.double().abs() @ w.double().abs().t() + b.double().abs()
@@ -78,6 +90,11 @@ def test_gemm_forward_and_input_gradient(prec, M, N, K):
     w2 = torch.randn(48, N, device="cuda", generator=g) * 0.1  # the next layer's weight [out, in]
     dy = torch.randn(M, 48, device="cuda", generator=g) / M
     ascale = 1.0 if prec == "x3" else float(2.0 ** 16)
+    if bits is None:  # the plain input-gradient form (the first layer's dx)
+        dx = x3.gemm(dy, x3.pack(w2, trans=True, prec=prec), ascale=ascale)
+        ref = dy.double() @ w2.double()
+        assert _rel_err(dx, ref, dy.double().abs() @ w2.double().abs()) < TOL[prec]
+        return
     cs = x3.colsum_buf(M, N, "cuda")
     dx = x3.gemm(dy, x3.pack(w2, trans=True, prec=prec), mbits_in=bits, colsum=cs, ascale=ascale)
     ref = (dy.double() @ w2.double()) * (y > 0)
