@@ -984,6 +984,17 @@ __global__ __launch_bounds__(256) void k_wg_reduce(const float* __restrict__ ws,
 // the blocks re-reading a unit's A rows do it through the same L2.  Waves
 // whose block is wider than CT take the sub-blocks of a unit in turn (A again
 // from L1 / L2).
+#ifndef BRES_WAVES
+#define BRES_WAVES 12
+#endif
+#ifndef BRES_BPREF
+#define BRES_BPREF 0
+#endif
+// waves per workgroup (one workgroup per CU: the B block fills LDS).  12 (168 registers per wave: no spills,
+// the epilogue's row offsets and both A buffers held) measured 5-8% faster than 16 (128 registers, spilling)
+// and than 8 (tools/bres_variants.sh + tools/bench_gemm_ab.py)
+constexpr int kBresWaves = BRES_WAVES;
+
 struct BresPlan {
     int xcds;   // XCDs the grid spreads over (8, or 1)
     int nblk;   // column blocks
@@ -1096,12 +1107,26 @@ __device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x
 // Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even).  ReLU bits:
 // bit 4 c + g of the tile-local word = bit 4 (tg0 + c) + g of the row tile's mask, i.e. local byte m is
 // global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD) whole bytes of its own tiles.
-template <int P, int CT, int EM, bool FULL>
-__device__ __forceinline__ void bres_epi(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
-                                         const Epi& ep, const float* sb, int lane) {
+// Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even), all stores
+// through buffer resources: rows past M fall past num_records and are dropped by the hardware, so there is
+// one code path with no per-element branches or 64-bit address arithmetic (lane offsets per row, the
+// column tile at an immediate offset); only a tile crossing N selects an out-of-range offset for its
+// lanes past N.  ReLU bits: bit 4 c + g of the tile-local words = bit 4 (tg0 + c) + g of the row tile's
+// mask, i.e. local byte m is global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD)
+// whole bytes of its own tiles.  Bits of rows past M are left unspecified (every reader masks by row);
+// columns past N compute to exact zeros (zero B rows and bias) and record 0.
+template <int P, int CT, int EM>
+__device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
+                                              const Epi& ep, __amdgpu_buffer_rsrc_t crs,
+                                              __amdgpu_buffer_rsrc_t srs, const float* sb, int lane) {
     constexpr int NW = (4 * CT + 31) / 32;  // local mask words
     int rq = 4 * (lane >> 4);
-    asm volatile("" : "+v"(rq));  // row addresses formed here, not hoisted over the main loop and held
+    asm volatile("" : "+v"(rq));  // offsets formed here, not hoisted over the main loop and held
+    const int row0 = 16 * rt + rq, cl = lane & 15;
+    uint32_t voff[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) voff[g] = 4u * ((uint32_t)(row0 + g) * (uint32_t)ep.ldc + (uint32_t)cl);
+    const int soff = 64 * tg0;  // bytes: the block's first column tile
     uint32_t lbits[NW];
 #pragma unroll
     for (int w = 0; w < NW; w++) lbits[w] = 0u;
@@ -1111,50 +1136,48 @@ __device__ __forceinline__ void bres_epi(const f32x4 (&acc)[CT], int rt, int tg0
 #pragma unroll
         for (int m = 0; m < (CT + 1) / 2; m++)
             if (2 * m < ctn) lbits[m >> 2] |= (uint32_t)mi[m] << (8 * (m & 3));
+        if (16 * rt + 16 > M) {  // the last row tile: rows past M masked out (their bits are unspecified)
+            uint32_t rm = 0u;
+#pragma unroll
+            for (int g = 0; g < 4; g++) rm |= (row0 + g < M ? 1u : 0u) << g;
+#pragma unroll
+            for (int w = 0; w < NW; w++) lbits[w] &= rm * 0x11111111u;
+        }
     }
-    const float* sbl = sb + (lane & 15);
-    // FULL: every row and column of the tile exists -- no per-element checks, one row pointer per g and
-    // the columns at immediate offsets
-    float* crow = ep.c + (size_t)(16 * rt + rq) * ep.ldc + 16 * tg0 + (lane & 15);
+    const float* sbl = sb + cl;
 #pragma unroll
     for (int c = 0; c < CT; c++) {
         if (c >= ctn || 16 * (tg0 + c) >= N) continue;  // wave-uniform (continue: the loop stays unrolled)
-        const int col = 16 * (tg0 + c) + (lane & 15);
+        const int col = 16 * (tg0 + c) + cl;
+        const bool part = 16 * (tg0 + c) + 16 > N;  // wave-uniform: a tile crossing N
         const float bv = (EM != EM_BWD && ep.bias) ? sbl[16 * c] : 0.f;
+        float cs = 0.f;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const int row = 16 * rt + rq + g, bit = 4 * c + g;
+            const int bit = 4 * c + g;
             float x = acc[c][g];
             if (P == P_F16) x *= ep.cscale;
             if (EM == EM_BWD) {
-                if (!((lbits[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
+                const bool on = (lbits[bit >> 5] >> (bit & 31)) & 1u;
+                if (!on) x = 0.f;
+                cs += x;
             } else {
                 x += bv;
                 if (ep.relu) x = fmaxf(x, 0.f);
-            }
-            if (FULL && 16 * (tg0 + c) + 16 <= N) {  // the whole tile inside N (wave-uniform)
                 if (EM == EM_FWD) lbits[bit >> 5] |= (x > 0.f ? 1u : 0u) << (bit & 31);
+            }
+            uint32_t o = voff[g] + 64u * c;
+            if (part && col >= N) o = kBufOOB;
 #ifdef BRES_NO_STORE  // diagnostic builds only
-                if (x == 1234.5f)
+            if (x == 1234.5f)
 #endif
-                crow[(size_t)g * ep.ldc + 16 * c] = x;
-            } else {
-                if (EM == EM_FWD && x > 0.f && col < N && row < M) lbits[bit >> 5] |= 1u << (bit & 31);
-                if (row < M && col < N) ep.c[(size_t)row * ep.ldc + col] = x;
-            }
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), crs, o, soff, 0);
         }
-        if (EM == EM_BWD && ep.colsum) {
-            float cs = 0.f;
-#pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const int row = 16 * rt + rq + g;
-                const float v = P == P_F16 ? acc[c][g] * ep.cscale : acc[c][g];
-                const int bit = 4 * c + g;
-                if ((FULL || row < M) && ((lbits[bit >> 5] >> (bit & 31)) & 1u)) cs += v;
-            }
+        if (EM == EM_BWD && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
             cs += __shfl_xor(cs, 16);
             cs += __shfl_xor(cs, 32);
-            if (lane < 16 && col < N && (FULL || 16 * rt < M)) ep.colsum[(size_t)rt * N + col] = cs;
+            const uint32_t so = (lane < 16 && col < N) ? 4u * ((uint32_t)rt * (uint32_t)N + (uint32_t)col) : kBufOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), srs, so, 0, 0);
         }
     }
     if (EM == EM_FWD) {
@@ -1163,15 +1186,6 @@ __device__ __forceinline__ void bres_epi(const f32x4 (&acc)[CT], int rt, int tg0
         for (int m = 0; m < (CT + 1) / 2; m++)
             if (2 * m < ctn) mb[m] = (uint8_t)(lbits[m >> 2] >> (8 * (m & 3)));
     }
-}
-
-template <int P, int CT, int EM>
-__device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
-                                              const Epi& ep, const float* sb, int lane) {
-    if (16 * rt + 16 <= M)  // wave-uniform; columns past N checked per tile
-        bres_epi<P, CT, EM, true>(acc, rt, tg0, ctn, M, N, ep, sb, lane);
-    else
-        bres_epi<P, CT, EM, false>(acc, rt, tg0, ctn, M, N, ep, sb, lane);
 }
 
 // one 32-wide k-step: cur -> fragments, step ks + 1 -> nxt (past the last step: offsets past K, zeros),
@@ -1188,6 +1202,23 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&c
     int boff = ((ks * ctb + c0) * np) * 64 + lane;  // bf16x8 units
     asm volatile("" : "+v"(boff));                  // one base per step (not 18 hoisted addresses)
     const bf16x8* bp = reinterpret_cast<const bf16x8*>(sF) + boff;
+#if BRES_BPREF
+    // column c + 1's B fragments read while column c's MFMAs run
+    bf16x8 bb[2][3];
+#pragma unroll
+    for (int q = 0; q < np; q++) bb[0][q] = bp[q * 64];
+#pragma unroll
+    for (int c = 0; c < CT; c++) {
+        if (c < ctn) {  // wave-uniform (a guard, not a break: the loop stays fully unrolled, acc in registers)
+            if (c + 1 < CT && c + 1 < ctn) {
+#pragma unroll
+                for (int q = 0; q < np; q++) bb[(c + 1) & 1][q] = bp[((c + 1) * np + q) * 64];
+            }
+#pragma unroll
+            for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb[c & 1], acc[r][c]);
+        }
+    }
+#else
 #pragma unroll
     for (int c = 0; c < CT; c++) {
         if (c < ctn) {  // wave-uniform (a guard, not a break: the loop stays fully unrolled, acc in registers)
@@ -1198,10 +1229,11 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&c
             for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb, acc[r][c]);
         }
     }
+#endif
 }
 
 template <int P, int CT, int RT, int EM, int VW>
-__global__ __launch_bounds__(kThreads) void k_bres(const float* __restrict__ A, int lda, float ascale,
+__global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restrict__ A, int lda, float ascale,
                                                    const uint16_t* __restrict__ B, int M, int N, int K, int nks,
                                                    BresPlan pl, Epi ep) {
     static_assert(EM == EM_F32 || EM == EM_FWD || EM == EM_BWD, "fp32 outputs");
@@ -1223,14 +1255,14 @@ __global__ __launch_bounds__(kThreads) void k_bres(const float* __restrict__ A, 
 
     // ---- the block of B -> LDS, once ----
     const int nF = ctb * nfull * np;
-    for (int p = wave; p < nF; p += kWaves) {
+    for (int p = wave; p < nF; p += kBresWaves) {
         const int q = p % np, cks = p / np, c = cks % ctb, ks = cks / ctb;
         const uint4* src =
             reinterpret_cast<const uint4*>(B + ((size_t)(t0 + c) * nks + ks) * Prec<P>::kBlk + q * 512);
         __builtin_amdgcn_global_load_lds(src + lane, sF + (size_t)p * 512, 16, 0, 0);
     }
     if (half) {
-        for (int p = wave; p < ctb * np; p += kWaves) {
+        for (int p = wave; p < ctb * np; p += kBresWaves) {
             const int q = p % np, c = p / np;
             const uint2* src =
                 reinterpret_cast<const uint2*>(B + ((size_t)(t0 + c) * nks + nfull) * Prec<P>::kBlk + q * 512);
@@ -1238,7 +1270,7 @@ __global__ __launch_bounds__(kThreads) void k_bres(const float* __restrict__ A, 
         }
     }
     if (EM != EM_BWD && ep.bias)
-        for (int t = threadIdx.x; t < ctb * 16; t += kThreads) {
+        for (int t = threadIdx.x; t < ctb * 16; t += 64 * kBresWaves) {
             const int col = 16 * t0 + t;
             sbias[t] = col < N ? ep.bias[col] : 0.f;
         }
@@ -1256,8 +1288,13 @@ __global__ __launch_bounds__(kThreads) void k_bres(const float* __restrict__ A, 
     // gfx9 buffer resource word 3 0x00020000: 32-bit data format, raw (stride 0) addressing
     const __amdgpu_buffer_rsrc_t arsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((size_t)M * lda * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t crs =  // C [M, ldc]: rows past M past num_records
+        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t srs =  // colsum [ceil(M / 16), N]
+        __builtin_amdgcn_make_buffer_rsrc((void*)ep.colsum, (short)0, (int)((size_t)((M + 15) / 16) * N * 4),
+                                          0x00020000);
     for (int t = 0;; t++) {
-        const int u = (x + X * (wb + nW * t)) * kWaves + wave;
+        const int u = (x + X * (wb + nW * t)) * kBresWaves + wave;
         if (u >= nu) break;
         BresA as;
         as.rsrc = arsrc;
@@ -1307,7 +1344,7 @@ __global__ __launch_bounds__(kThreads) void k_bres(const float* __restrict__ A, 
             }
 #pragma unroll
             for (int r = 0; r < RT; r++)
-                bres_epilogue<P, CT, EM>(acc[r], RT * u + r, t0 + c0, ctn, M, N, ep, sbias + 16 * c0, lane);
+                bres_epilogue<P, CT, EM>(acc[r], RT * u + r, t0 + c0, ctn, M, N, ep, crs, srs, sbias + 16 * c0, lane);
         }
         X3_STAMP(1 + t, 2, __builtin_amdgcn_s_memtime());  // end of unit t
     }
@@ -1459,8 +1496,10 @@ enum { C_NARROW = 0, C_WIDE = 1 };
 template <int C> struct BresCfg { static constexpr int CT = C == C_NARROW ? 6 : 17, RT = C == C_NARROW ? 2 : 1; };
 
 // The column blocks and the per-XCD workgroup split (see k_bres); false: the shape does not fit.
-static bool bres_plan(int prec, int M, int N, int K, int lda, bool bits, BresPlan& pl, int& cfg) {
-    if (M < kBresMinRows || (size_t)M * lda * 4 >= ((size_t)1 << 31)) return false;  // A through a buffer resource
+static bool bres_plan(int prec, int M, int N, int K, int lda, int ldc, bool bits, BresPlan& pl, int& cfg) {
+    // A and C through buffer resources (num_records < 2^31, in-range offsets < 2^31 = kBufOOB)
+    if (M < kBresMinRows || (size_t)M * lda * 4 >= ((size_t)1 << 31) || (size_t)(M + 16) * ldc * 4 >= ((size_t)1 << 31))
+        return false;
     const int np = prec == MM_PREC_X3 ? 3 : 1;
     const int tiles = (N + 15) / 16;
     const int nks = rup(K, 32) / 32, rem = K % 32;
@@ -1516,7 +1555,7 @@ static int launch_bres(const float* a, int lda, float ascale, const uint16_t* b,
     }
     constexpr int np = Prec<P>::kPlanes;
     const size_t lds = (size_t)pl.ctb * np * (pl.nfull * 1024 + pl.half * 512) + (size_t)pl.ctb * 16 * 4;
-    hipLaunchKernelGGL((k_bres<P, CT, RT, EM, VW>), dim3(persistent_grid()), dim3(kThreads), lds, s, a, lda, ascale, b,
+    hipLaunchKernelGGL((k_bres<P, CT, RT, EM, VW>), dim3(persistent_grid()), dim3(64 * kBresWaves), lds, s, a, lda, ascale, b,
                        M, N, K, rup(K, 32) / 32, pl, ep);
     return (int)hipGetLastError();
 }
@@ -1575,14 +1614,14 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
     if (M == 0) return 0;
     Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale};
     hipStream_t s = (hipStream_t)stream;
-    // the B-resident kernel where it measured faster (tools/bench_gemm_ab.py): 16-byte rows, and for
-    // f16 not the input-gradient form (its 17-tile epilogue spills: at par with the streaming kernel)
     BresPlan pl;
     int cfg = C_NARROW;
-    if (!mask && !c_tp && v4 && !(prec == MM_PREC_F16 && mbits_in) && bres_enabled() &&
-        bres_plan(prec, M, N, K, lda, mbits_in || mbits_out, pl, cfg)) {
-        if (prec == MM_PREC_X3) return dispatch_bres<P_X3, 4>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s);
-        return dispatch_bres<P_F16, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s);
+    if (!mask && !c_tp && bres_enabled() && bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) {
+        if (prec == MM_PREC_X3)
+            return v4 ? dispatch_bres<P_X3, 4>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s)
+                      : dispatch_bres<P_X3, 2>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s);
+        return v4 ? dispatch_bres<P_F16, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s)
+                  : dispatch_bres<P_F16, 2>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s);
     }
     if (prec == MM_PREC_X3)
         return v4 ? dispatch_nt<P_X3, ASrcF32>(a, lda, 1.f, b_tp, M, N, K, ep, s)
