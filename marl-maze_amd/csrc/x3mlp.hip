@@ -195,6 +195,7 @@ struct Epi {
     float* colsum;           // EM_BWD, or null: per row tile column sums of the output [rows / 16][N]
     int ldc, ldm, relu, cnks;  // cnks = TP column blocks of the output (ceil(N / 32))
     float cscale;              // P_F16: out = acc * cscale before bias (the inverse of the A scale)
+    int bufok;                 // fp32 c (and colsum) addressable through buffer resources (< 2^31 bytes)
 };
 
 // B piece i (column tile i / planes, plane i % planes) of k-step ks -> LDS (one 1-KiB LDS-DMA)
@@ -457,6 +458,89 @@ __device__ __forceinline__ void epilogue_tp(const f32x4 (&acc)[NT], float* slice
 // DMA issues spread over the MFMA stream.  One barrier per k-step; four waves
 // per SIMD hide the LDS latency of the B fragment reads.  Persistent over
 // 256-row units.
+constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past every buffer (num_records < 2^31)
+
+// Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even), all stores
+// through buffer resources: rows past M fall past num_records and are dropped by the hardware, so there is
+// one code path with no per-element branches or 64-bit address arithmetic (lane offsets per row, the
+// column tile at an immediate offset); only a tile crossing N selects an out-of-range offset for its
+// lanes past N.  ReLU bits: bit 4 c + g of the tile-local words = bit 4 (tg0 + c) + g of the row tile's
+// mask, i.e. local byte m is global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD)
+// whole bytes of its own tiles.  Bits of rows past M are left unspecified (every reader masks by row);
+// columns past N compute to exact zeros (zero B rows and bias) and record 0.
+template <int P, int CT, int EM>
+__device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
+                                              const Epi& ep, __amdgpu_buffer_rsrc_t crs,
+                                              __amdgpu_buffer_rsrc_t srs, const float* sb, int lane) {
+    constexpr int NW = (4 * CT + 31) / 32;  // local mask words
+    int rq = 4 * (lane >> 4);
+    asm volatile("" : "+v"(rq));  // offsets formed here, not hoisted over the main loop and held
+    const int row0 = 16 * rt + rq, cl = lane & 15;
+    uint32_t voff[4];
+#pragma unroll
+    for (int g = 0; g < 4; g++) voff[g] = 4u * ((uint32_t)(row0 + g) * (uint32_t)ep.ldc + (uint32_t)cl);
+    const int soff = 64 * tg0;  // bytes: the block's first column tile
+    uint32_t lbits[NW];
+#pragma unroll
+    for (int w = 0; w < NW; w++) lbits[w] = 0u;
+    if (EM == EM_BWD) {
+        const uint8_t* mi =
+            reinterpret_cast<const uint8_t*>(ep.mbits_in + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
+#pragma unroll
+        for (int m = 0; m < (CT + 1) / 2; m++)
+            if (2 * m < ctn) lbits[m >> 2] |= (uint32_t)mi[m] << (8 * (m & 3));
+        if (16 * rt + 16 > M) {  // the last row tile: rows past M masked out (their bits are unspecified)
+            uint32_t rm = 0u;
+#pragma unroll
+            for (int g = 0; g < 4; g++) rm |= (row0 + g < M ? 1u : 0u) << g;
+#pragma unroll
+            for (int w = 0; w < NW; w++) lbits[w] &= rm * 0x11111111u;
+        }
+    }
+    const float* sbl = sb + cl;
+#pragma unroll
+    for (int c = 0; c < CT; c++) {
+        if (c >= ctn || 16 * (tg0 + c) >= N) continue;  // wave-uniform (continue: the loop stays unrolled)
+        const int col = 16 * (tg0 + c) + cl;
+        const bool part = 16 * (tg0 + c) + 16 > N;  // wave-uniform: a tile crossing N
+        const float bv = (EM != EM_BWD && ep.bias) ? sbl[16 * c] : 0.f;
+        float cs = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int bit = 4 * c + g;
+            float x = acc[c][g];
+            if (P == P_F16) x *= ep.cscale;
+            if (EM == EM_BWD) {
+                const bool on = (lbits[bit >> 5] >> (bit & 31)) & 1u;
+                if (!on) x = 0.f;
+                cs += x;
+            } else {
+                x += bv;
+                if (ep.relu) x = fmaxf(x, 0.f);
+                if (EM == EM_FWD) lbits[bit >> 5] |= (x > 0.f ? 1u : 0u) << (bit & 31);
+            }
+            uint32_t o = voff[g] + 64u * c;
+            if (part && col >= N) o = kBufOOB;
+#ifdef BRES_NO_STORE  // diagnostic builds only
+            if (x == 1234.5f)
+#endif
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), crs, o, soff, 0);
+        }
+        if (EM == EM_BWD && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
+            cs += __shfl_xor(cs, 16);
+            cs += __shfl_xor(cs, 32);
+            const uint32_t so = (lane < 16 && col < N) ? 4u * ((uint32_t)rt * (uint32_t)N + (uint32_t)col) : kBufOOB;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), srs, so, 0, 0);
+        }
+    }
+    if (EM == EM_FWD) {
+        uint8_t* mb = reinterpret_cast<uint8_t*>(ep.mbits_out + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
+#pragma unroll
+        for (int m = 0; m < (CT + 1) / 2; m++)
+            if (2 * m < ctn) mb[m] = (uint8_t)(lbits[m >> 2] >> (8 * (m & 3)));
+    }
+}
+
 #ifdef X3_STAMPS  // diagnostic builds only (tools/x3_stamps.sh): per-wave phase clocks of k_x3nt
 __device__ unsigned long long g_x3_stamps[256 * 16 * kWaves * 8];
 #define X3_STAMP(it, slot, val)                                                                       \
@@ -483,6 +567,11 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
     __shared__ __attribute__((aligned(16))) uint16_t sB1[C::kStageB];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // (unused when !ep.bufok: then the ranges below are not consulted)
+    const __amdgpu_buffer_rsrc_t crs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)ep.colsum, (short)0, (int)((size_t)((M + 15) / 16) * N * 4), 0x00020000);
     // workgroup g takes units g, g + G, ...  XCD-aware unit order: units u and
     // u + 8 (one XCD) are the column blocks of one row block, so its A is shared
     // through that XCD's L2
@@ -526,10 +615,14 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         X3_STAMP(it, 2, __builtin_amdgcn_s_memtime());
 
         // ---- epilogue (after the last k-step's barrier both stage buffers are free) ----
-        if constexpr (EM == EM_TP)
+        if constexpr (EM == EM_TP) {
             epilogue_tp<NT>(acc, reinterpret_cast<float*>(sB0) + wave * 16 * 36, rt, M, N, ep, lane);
-        else
-            epilogue_f32<NT, EM, P>(acc, rt, M, N, cb * 16 * NT, ep, sbias, lane);
+        } else {
+            if (ep.bufok && !ep.mask)  // buffer stores, one code path (bres_epilogue; tiles cb NT .. : even when bits)
+                bres_epilogue<P, NT, EM>(acc, rt, cb * NT, NT, M, N, ep, crs, srs, sbias, lane);
+            else
+                epilogue_f32<NT, EM, P>(acc, rt, M, N, cb * 16 * NT, ep, sbias, lane);
+        }
         // the next unit's DMA overwrites the epilogue slices: LDS reads done everywhere
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
@@ -1012,7 +1105,6 @@ constexpr int kBresMaxBlk = 8;
 // at the end of the step that issued them: no prefetch at all)
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
-constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past every buffer (num_records < 2^31)
 
 struct BresA {
     __amdgpu_buffer_rsrc_t rsrc;  // A: base, num_records = M lda 4 bytes
@@ -1107,87 +1199,6 @@ __device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x
 // Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even).  ReLU bits:
 // bit 4 c + g of the tile-local word = bit 4 (tg0 + c) + g of the row tile's mask, i.e. local byte m is
 // global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD) whole bytes of its own tiles.
-// Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even), all stores
-// through buffer resources: rows past M fall past num_records and are dropped by the hardware, so there is
-// one code path with no per-element branches or 64-bit address arithmetic (lane offsets per row, the
-// column tile at an immediate offset); only a tile crossing N selects an out-of-range offset for its
-// lanes past N.  ReLU bits: bit 4 c + g of the tile-local words = bit 4 (tg0 + c) + g of the row tile's
-// mask, i.e. local byte m is global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD)
-// whole bytes of its own tiles.  Bits of rows past M are left unspecified (every reader masks by row);
-// columns past N compute to exact zeros (zero B rows and bias) and record 0.
-template <int P, int CT, int EM>
-__device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, int tg0, int ctn, int M, int N,
-                                              const Epi& ep, __amdgpu_buffer_rsrc_t crs,
-                                              __amdgpu_buffer_rsrc_t srs, const float* sb, int lane) {
-    constexpr int NW = (4 * CT + 31) / 32;  // local mask words
-    int rq = 4 * (lane >> 4);
-    asm volatile("" : "+v"(rq));  // offsets formed here, not hoisted over the main loop and held
-    const int row0 = 16 * rt + rq, cl = lane & 15;
-    uint32_t voff[4];
-#pragma unroll
-    for (int g = 0; g < 4; g++) voff[g] = 4u * ((uint32_t)(row0 + g) * (uint32_t)ep.ldc + (uint32_t)cl);
-    const int soff = 64 * tg0;  // bytes: the block's first column tile
-    uint32_t lbits[NW];
-#pragma unroll
-    for (int w = 0; w < NW; w++) lbits[w] = 0u;
-    if (EM == EM_BWD) {
-        const uint8_t* mi =
-            reinterpret_cast<const uint8_t*>(ep.mbits_in + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
-#pragma unroll
-        for (int m = 0; m < (CT + 1) / 2; m++)
-            if (2 * m < ctn) lbits[m >> 2] |= (uint32_t)mi[m] << (8 * (m & 3));
-        if (16 * rt + 16 > M) {  // the last row tile: rows past M masked out (their bits are unspecified)
-            uint32_t rm = 0u;
-#pragma unroll
-            for (int g = 0; g < 4; g++) rm |= (row0 + g < M ? 1u : 0u) << g;
-#pragma unroll
-            for (int w = 0; w < NW; w++) lbits[w] &= rm * 0x11111111u;
-        }
-    }
-    const float* sbl = sb + cl;
-#pragma unroll
-    for (int c = 0; c < CT; c++) {
-        if (c >= ctn || 16 * (tg0 + c) >= N) continue;  // wave-uniform (continue: the loop stays unrolled)
-        const int col = 16 * (tg0 + c) + cl;
-        const bool part = 16 * (tg0 + c) + 16 > N;  // wave-uniform: a tile crossing N
-        const float bv = (EM != EM_BWD && ep.bias) ? sbl[16 * c] : 0.f;
-        float cs = 0.f;
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const int bit = 4 * c + g;
-            float x = acc[c][g];
-            if (P == P_F16) x *= ep.cscale;
-            if (EM == EM_BWD) {
-                const bool on = (lbits[bit >> 5] >> (bit & 31)) & 1u;
-                if (!on) x = 0.f;
-                cs += x;
-            } else {
-                x += bv;
-                if (ep.relu) x = fmaxf(x, 0.f);
-                if (EM == EM_FWD) lbits[bit >> 5] |= (x > 0.f ? 1u : 0u) << (bit & 31);
-            }
-            uint32_t o = voff[g] + 64u * c;
-            if (part && col >= N) o = kBufOOB;
-#ifdef BRES_NO_STORE  // diagnostic builds only
-            if (x == 1234.5f)
-#endif
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), crs, o, soff, 0);
-        }
-        if (EM == EM_BWD && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
-            cs += __shfl_xor(cs, 16);
-            cs += __shfl_xor(cs, 32);
-            const uint32_t so = (lane < 16 && col < N) ? 4u * ((uint32_t)rt * (uint32_t)N + (uint32_t)col) : kBufOOB;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), srs, so, 0, 0);
-        }
-    }
-    if (EM == EM_FWD) {
-        uint8_t* mb = reinterpret_cast<uint8_t*>(ep.mbits_out + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
-#pragma unroll
-        for (int m = 0; m < (CT + 1) / 2; m++)
-            if (2 * m < ctn) mb[m] = (uint8_t)(lbits[m >> 2] >> (8 * (m & 3)));
-    }
-}
-
 // one 32-wide k-step: cur -> fragments, step ks + 1 -> nxt (past the last step: offsets past K, zeros),
 // the CT column tiles' MFMAs for both row tiles (each B fragment read feeds both)
 template <int P, int CT, int RT, int VW>
@@ -1593,7 +1604,8 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
     if (e) return e;
     if (!a_tp || ((uintptr_t)a_tp & 15)) return MM_E_ARG;
     if (M == 0) return 0;
-    Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32, 1.f};
+    Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32, 1.f,
+           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31)};
     return dispatch_nt<P_X3, ASrcTP>(a_tp, 0, 1.f, b_tp, M, N, K, ep, (hipStream_t)stream);
 }
 
@@ -1612,7 +1624,8 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
     if (mbits_in && (bias || relu)) return MM_E_ARG;  // the input-gradient form: no bias, no ReLU of its own
     if (colsum && (!mbits_in || !c)) return MM_E_ARG;
     if (M == 0) return 0;
-    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale};
+    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale,
+           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31) && (size_t)((M + 15) / 16) * N * 4 < ((size_t)1 << 31)};
     hipStream_t s = (hipStream_t)stream;
     BresPlan pl;
     int cfg = C_NARROW;
