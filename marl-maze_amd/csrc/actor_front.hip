@@ -131,29 +131,31 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a . b over N (even) values, b in LDS: two interleaved accumulators (even / odd k) on packed FMAs
+// (v_pk_fma_f32: two FMAs per instruction, half the dependent chain), summed at the end.  The
+// summation order is not the reference's (torch's CPU einsum order is not reproducible anyway; the
+// front-end is held to fp64 / torch within 1e-5).
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 template <int N>
 __device__ __forceinline__ float dot4(const float* a, const float* __restrict__ b_lds) {  // N % 2 == 0
-    float acc = 0.f;
+    f32x2 acc = {0.f, 0.f};
     if constexpr (N % 4 == 0) {
         const float4* b4 = reinterpret_cast<const float4*>(b_lds);
 #pragma unroll
         for (int k = 0; k < N / 4; k++) {
             const float4 v = b4[k];
-            acc = fmaf(a[4 * k], v.x, acc);
-            acc = fmaf(a[4 * k + 1], v.y, acc);
-            acc = fmaf(a[4 * k + 2], v.z, acc);
-            acc = fmaf(a[4 * k + 3], v.w, acc);
+            acc = __builtin_elementwise_fma(f32x2{a[4 * k], a[4 * k + 1]}, f32x2{v.x, v.y}, acc);
+            acc = __builtin_elementwise_fma(f32x2{a[4 * k + 2], a[4 * k + 3]}, f32x2{v.z, v.w}, acc);
         }
     } else {
         const float2* b2 = reinterpret_cast<const float2*>(b_lds);
 #pragma unroll
         for (int k = 0; k < N / 2; k++) {
             const float2 v = b2[k];
-            acc = fmaf(a[2 * k], v.x, acc);
-            acc = fmaf(a[2 * k + 1], v.y, acc);
+            acc = __builtin_elementwise_fma(f32x2{a[2 * k], a[2 * k + 1]}, f32x2{v.x, v.y}, acc);
         }
     }
-    return acc;
+    return acc.x + acc.y;
 }
 
 template <int N>

@@ -6,6 +6,8 @@ with a small absolute floor (1e-6) for values that are ~0 (the actor loss of a
 normalised advantage batch).  Parameters after Adam are compared at the scale
 of one Adam step in test_gpu_update_parity.py (with per-parameter gradients).
 """
+import copy
+
 import numpy as np
 import pytest
 import torch
@@ -189,11 +191,24 @@ def test_fused_front_matches_torch(parity, algo, monkeypatch):
     params = front_params(pr, at)
     href = at(pr(x))
     gref = torch.autograd.grad(href, params, dh)
+    # fp64 truth: the fused kernels' summation order differs from torch's (both are fp32 roundings of it)
+    a64 = copy.deepcopy(actor).double()
+    p64 = front_params(a64.projection, a64.attention)
+    h64 = a64.attention(a64.projection(x.double()))
+    g64 = torch.autograd.grad(h64, p64, dh.double())
     h = _FusedFront.apply(x, parity, *params)
     # weights x3: large attention logits amplify summation-order differences
-    np.testing.assert_allclose(h.detach().cpu().numpy(), href.detach().cpu().numpy(), rtol=1e-4, atol=2e-4)
+    e_ours = (h.double() - h64).abs().max().item()
+    e_torch = (href.double() - h64).abs().max().item()
+    assert e_ours <= 2.0 * e_torch + 1e-6, (e_ours, e_torch)
+    np.testing.assert_allclose(h.detach().cpu().numpy(), href.detach().cpu().numpy(), rtol=1e-4, atol=5e-4)
     g = torch.autograd.grad(h, params, dh)
-    for a, b in zip(g, gref):
+    for a, b, t in zip(g, gref, g64):
+        e_ours = (a.double() - t).abs().max().item()
+        e_torch = (b.double() - t).abs().max().item()
+        # within torch's own fp32 error or 1e-5 of the tensor's max (the kernel's long fp32 sums over
+        # samples are fixed-order and serial per thread; torch reduces pairwise)
+        assert e_ours <= max(2.0 * e_torch, 1e-5 * t.abs().max().item()), (e_ours, e_torch)
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-3 * b.abs().max().item())
 
 
