@@ -298,12 +298,14 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
                 s[j] = div_sqrt_kq(dot4<kKq>(q, Ks[g][j]));
                 mx = fmaxf(mx, s[j]);
             }
-            float sum = 0.f;
+            float sum0 = 0.f, sum1 = 0.f;  // even / odd j: two short chains (the backward recomputes the same way)
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
                 s[j] = expf(s[j] - mx);
-                sum += s[j];
+                if (j & 1) sum1 += s[j];
+                else sum0 += s[j];
             }
+            const float sum = sum0 + sum1;
             float out[kEmb];
 #pragma unroll
             for (int c = 0; c < kEmb; c++) out[c] = 0.f;
@@ -443,21 +445,25 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
                 p[j] = div_sqrt_kq(dot4<kKq>(q, my + kOffK + j * kKq));
                 mx = fmaxf(mx, p[j]);
             }
-            float sum = 0.f;
+            float sum0 = 0.f, sum1 = 0.f;  // as the forward: even / odd j
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
                 p[j] = expf(p[j] - mx);
-                sum += p[j];
+                if (j & 1) sum1 += p[j];
+                else sum0 += p[j];
             }
+            const float sum = sum0 + sum1;
             float dp[kTok];
-            float rs = 0.f;
+            float rs0 = 0.f, rs1 = 0.f;
             const float inv = 1.f / sum;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
                 p[j] = p[j] * inv;
                 dp[j] = dot4<kEmb>(dctx, my + kOffV + j * kEmb);  // dP_ij = dctx_i . v_j
-                rs = fmaf(dp[j], p[j], rs);
+                if (j & 1) rs1 = fmaf(dp[j], p[j], rs1);
+                else rs0 = fmaf(dp[j], p[j], rs0);
             }
+            const float rs = rs0 + rs1;
 #pragma unroll
             for (int a = 0; a < kKq; a++) dq[a] = 0.f;
 #pragma unroll

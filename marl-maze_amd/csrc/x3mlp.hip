@@ -890,33 +890,37 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     const float* const baseA = dy + (size_t)m_begin * lddy;
     const float* const baseB = x + (size_t)m_begin * ldx + col0;
 
-    int r8[kPer], goff[kPer], loff[kPer];
-    bool ok[kPer];
+    // loads through buffer resources over the slice's remaining rows: rows past the slice and columns
+    // past N / K (an out-of-range offset) read zeros -- no per-element branch or 64-bit address (the
+    // exec-masked conditional loads cost ~6 instructions each)
+    int loff[kPer];
+    uint32_t voff[kPer];
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
         const int e = threadIdx.x + kWgThreads * q;
         const bool isA = e < itemsA;
         const int e2 = isA ? e : e - itemsA, w = isA ? 16 * TN : 16 * NTK;
         const int c = e2 / w, j = e2 - c * w;
-        ok[q] = e < items && (isA ? j < N : col0 + j < K);
-        r8[q] = 8 * c;
-        goff[q] = ok[q] ? 8 * c * (isA ? lddy : ldx) + j : 0;
+        const bool ok = e < items && (isA ? j < N : col0 + j < K);
+        voff[q] = ok ? 4u * (uint32_t)(8 * c * (isA ? lddy : ldx) + j) : kBufOOB;
         loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
     }
     float raw[kPer][8];
     auto load_piece = [&](int q, int r0) {
-        const bool isA = threadIdx.x + kWgThreads * q < itemsA;  // wave-uniform (itemsA = 64 TN)
+        // wave-uniform (itemsA = 64 TN), made scalar: a resource built from a divergent value becomes a
+        // readfirstlane waterfall loop per load
+        const bool isA = __builtin_amdgcn_readfirstlane(threadIdx.x + kWgThreads * q) < itemsA;
         const int ld = isA ? lddy : ldx;
-        const float* rowp = (isA ? baseA : baseB) + (size_t)r0 * ld;
-        int o = goff[q];
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((isA ? baseA : baseB) + (size_t)r0 * ld), (short)0, (int)((nrows - r0) * ld * 4), 0x00020000);
+        uint32_t o = voff[q];
         asm volatile("" : "+v"(o));
-        const int lim = nrows - r0 - r8[q];
 #pragma unroll
         for (int i = 0; i < 8; i++) {
 #ifdef WG_NO_GLOAD
-            raw[q][i] = ok[q] ? (float)(r0 + i) : 0.f;
+            raw[q][i] = o < kBufOOB ? (float)(r0 + i) : 0.f;
 #else
-            raw[q][i] = (ok[q] && i < lim) ? rowp[o + i * ld] : 0.f;
+            raw[q][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u * i * ld, 0, 0));
 #endif
         }
     };
@@ -1201,7 +1205,7 @@ __device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x
 // global byte tg0 / 2 + m -- each block writes (EM_FWD) and reads (EM_BWD) whole bytes of its own tiles.
 // one 32-wide k-step: cur -> fragments, step ks + 1 -> nxt (past the last step: offsets past K, zeros),
 // the CT column tiles' MFMAs for both row tiles (each B fragment read feeds both)
-template <int P, int CT, int RT, int VW>
+template <int P, int CT, int RT, int VW, int D = 1>
 __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&cur)[RT][2], float4 (&nxt)[RT][2],
                                           const BresA& as, int ks, int K, int kq, int ctb, int c0, int ctn,
                                           float ascale, const uint16_t* sF, int lane) {
@@ -1209,7 +1213,7 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&c
     bf16x8 a[RT][3];
 #pragma unroll
     for (int r = 0; r < RT; r++) bres_frag<P>(cur[r], ascale, a[r]);
-    bres_load<RT, VW>(as, ks + 1, K, kq, nxt);
+    bres_load<RT, VW>(as, ks + D, K, kq, nxt);  // D steps ahead (past the last step: zeros)
     int boff = ((ks * ctb + c0) * np) * 64 + lane;  // bf16x8 units
     asm volatile("" : "+v"(boff));                  // one base per step (not 18 hoisted addresses)
     const bf16x8* bp = reinterpret_cast<const bf16x8*>(sF) + boff;
@@ -1325,22 +1329,45 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
             for (int r = 0; r < RT; r++)
 #pragma unroll
                 for (int c = 0; c < CT; c++) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-            // two A buffers, steps in pairs: step ks splits cur and loads step ks + 1 into nxt, so the
-            // loads stay in flight over a whole step (one buffer made the compiler copy at the loop end,
-            // waiting for the loads it had just issued)
-            float4 rawA[RT][2], rawB[RT][2];
-            bres_load<RT, VW>(as, 0, K, kq, rawA);
-            int ks = 0;
-            for (; ks + 2 <= nfull; ks += 2) {
-                bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
-                bres_step<P, CT, RT, VW>(acc, rawB, rawA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
-            }
-            const bool odd = ks < nfull;
-            if (odd) bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
-            if (half) {
-                uint2 a4[RT][3];
+            // A register buffers: step ks splits cur and loads a later step into another buffer, so the
+            // loads stay in flight over whole steps (one buffer made the compiler copy at the loop end,
+            // waiting for the loads it had just issued).  RT = 2 (x3): two buffers, one step ahead; RT = 1
+            // (f16, bound by its A loads): three buffers, two steps ahead.
+            uint2 a4[RT][3];
+            if constexpr (RT == 1) {
+                float4 rA[RT][2], rB[RT][2], rC[RT][2];
+                bres_load<RT, VW>(as, 0, K, kq, rA);
+                bres_load<RT, VW>(as, 1, K, kq, rB);
+                int ks = 0;
+                for (; ks + 3 <= nfull; ks += 3) {
+                    bres_step<P, CT, RT, VW, 2>(acc, rA, rC, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW, 2>(acc, rB, rA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW, 2>(acc, rC, rB, as, ks + 2, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                }
+                const int rem = nfull - ks;  // A holds step ks, B step ks + 1
+                if (rem >= 1) bres_step<P, CT, RT, VW, 2>(acc, rA, rC, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                if (rem >= 2) bres_step<P, CT, RT, VW, 2>(acc, rB, rA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                if (half) {  // step nfull is in A (rem 0), B (rem 1) or C (rem 2)
 #pragma unroll
-                for (int r = 0; r < RT; r++) bres_frag16<P>(odd ? rawB[r][0] : rawA[r][0], ascale, a4[r]);
+                    for (int r = 0; r < RT; r++)
+                        bres_frag16<P>(rem == 0 ? rA[r][0] : rem == 1 ? rB[r][0] : rC[r][0], ascale, a4[r]);
+                }
+            } else {
+                float4 rawA[RT][2], rawB[RT][2];
+                bres_load<RT, VW>(as, 0, K, kq, rawA);
+                int ks = 0;
+                for (; ks + 2 <= nfull; ks += 2) {
+                    bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW>(acc, rawB, rawA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                }
+                const bool odd = ks < nfull;
+                if (odd) bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                if (half) {
+#pragma unroll
+                    for (int r = 0; r < RT; r++) bres_frag16<P>(odd ? rawB[r][0] : rawA[r][0], ascale, a4[r]);
+                }
+            }
+            if (half) {
                 const uint2* bp = reinterpret_cast<const uint2*>(sT) + (size_t)(c0 * np) * 64 + lane;
 #pragma unroll
                 for (int c = 0; c < CT; c++) {
@@ -1778,6 +1805,8 @@ static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int ldd
 #ifdef WG_GENERIC  // diagnostic builds: the generic kernel for every shape
     return 1;
 #endif
+    if ((size_t)M * lddy * 4 >= ((size_t)1 << 31) || (size_t)M * ldx * 4 >= ((size_t)1 << 31))
+        return 1;  // loads through buffer resources (num_records < 2^31): the generic kernel
     return prec == MM_PREC_X3 ? launch_rect_p<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
                               : launch_rect_p<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
 }
