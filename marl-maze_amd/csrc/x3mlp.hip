@@ -221,6 +221,10 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& h, uint32_t
     l = __builtin_bit_cast(uint32_t, lb);
 }
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
+constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past every buffer (num_records < 2^31)
+
 // A operand sources.  A wave owns one row tile; per k-step each lane needs the
 // 8 values (row 16 rt + (l & 15), k 32 ks + 8 (l >> 4) .. +7) as three bf16x8.
 struct ASrcTP {  // pre-split TP planes: three lane-linear 1-KiB loads
@@ -250,31 +254,34 @@ struct ASrcTP {  // pre-split TP planes: three lane-linear 1-KiB loads
 template <int VW>
 struct ASrcF32V {
     typedef float4 Raw[2];
-    const float* row;  // this lane's row (clamped inside the matrix), column 4 (l >> 4)
-    int K, ok;         // ok: the row exists
+    __amdgpu_buffer_rsrc_t rs;  // A [M, lda] (the host keeps M lda 4 < 2^31: row chunks)
+    uint32_t roff;              // this lane's row (clamped inside the matrix), column 4 (l >> 4), bytes
+    int K, kq;
     float scale;
     __device__ void init(const float* base, int rt, int, int M, int lda, int K_, float scale_) {
         const int lane = threadIdx.x & 63;
-        const int r = 16 * rt + (lane & 15);
-        ok = r < M;
+        const int r = min(16 * rt + (lane & 15), M - 1);  // rows past M: computed, never stored
         K = K_;
         scale = scale_;
-        row = base + (size_t)(ok ? r : 0) * lda + 4 * (lane >> 4);
+        kq = 4 * (lane >> 4);
+        rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((size_t)M * lda * 4), 0x00020000);
+        roff = 4u * ((uint32_t)r * (uint32_t)lda + (uint32_t)kq);
     }
-    __device__ __forceinline__ void load(int ks, Raw& r, int lane) const {
-        const int k = 32 * ks + 4 * (lane >> 4);  // kcol(c, 0..3) = 4c.., kcol(c, 4..7) = 16 + 4c..
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (VW == 4) {
-            r[0] = (ok && k < K) ? *reinterpret_cast<const float4*>(row + 32 * ks) : z;
-            r[1] = (ok && k + 16 < K) ? *reinterpret_cast<const float4*>(row + 32 * ks + 16) : z;
-        } else {
+    // columns past K: an out-of-range offset reads zeros (no exec-masked conditional loads)
+    __device__ __forceinline__ void load(int ks, Raw& r, int) const {
+        const int k = 32 * ks + kq;  // kcol(c, 0..3) = 4c.., kcol(c, 4..7) = 16 + 4c..
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const float* p = row + 32 * ks + 16 * h;
-                const int kk = k + 16 * h;
-                const float2 a = (ok && kk < K) ? *reinterpret_cast<const float2*>(p) : make_float2(0.f, 0.f);
-                const float2 b = (ok && kk + 2 < K) ? *reinterpret_cast<const float2*>(p + 2) : make_float2(0.f, 0.f);
-                r[h] = make_float4(a.x, a.y, b.x, b.y);
+        for (int h = 0; h < 2; h++) {
+            const uint32_t o = roff + 4u * (32 * ks + 16 * h);
+            if constexpr (VW == 4) {
+                const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(rs, k + 16 * h < K ? o : kBufOOB, 0, 0);
+                r[h] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z),
+                                   __uint_as_float(v.w));
+            } else {
+                const u32x2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, k + 16 * h < K ? o : kBufOOB, 0, 0);
+                const u32x2v y = __builtin_amdgcn_raw_buffer_load_b64(rs, k + 16 * h + 2 < K ? o + 8 : kBufOOB, 0, 0);
+                r[h] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(y.x),
+                                   __uint_as_float(y.y));
             }
         }
     }
@@ -458,8 +465,6 @@ __device__ __forceinline__ void epilogue_tp(const f32x4 (&acc)[NT], float* slice
 // DMA issues spread over the MFMA stream.  One barrier per k-step; four waves
 // per SIMD hide the LDS latency of the B fragment reads.  Persistent over
 // 256-row units.
-constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past every buffer (num_records < 2^31)
-
 // Epilogue of one row tile x ctn column tiles (global tiles tg0 .. tg0 + ctn - 1; tg0 even), all stores
 // through buffer resources: rows past M fall past num_records and are dropped by the hardware, so there is
 // one code path with no per-element branches or 64-bit address arithmetic (lane offsets per row, the
@@ -1107,8 +1112,6 @@ constexpr int kBresMaxBlk = 8;
 // columns past K cost one select of the offset -- no branch, and no wait on the loaded value (a select
 // on the value, or two load forms merged at a branch, made the compiler wait for each k-step's loads
 // at the end of the step that issued them: no prefetch at all)
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
-typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
 
 struct BresA {
     __amdgpu_buffer_rsrc_t rsrc;  // A: base, num_records = M lda 4 bytes
@@ -1651,8 +1654,25 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
     if (mbits_in && (bias || relu)) return MM_E_ARG;  // the input-gradient form: no bias, no ReLU of its own
     if (colsum && (!mbits_in || !c)) return MM_E_ARG;
     if (M == 0) return 0;
-    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale,
-           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31) && (size_t)((M + 15) / 16) * N * 4 < ((size_t)1 << 31)};
+    // the kernels address A and C through buffer resources (num_records < 2^31 bytes): larger calls run
+    // in row chunks of a multiple of 256 rows (whole row tiles of the bit masks and column sums)
+    const size_t wmax = std::max(std::max((size_t)lda, (size_t)ldc), std::max((size_t)ldm, (size_t)N));
+    const size_t cap = ((((size_t)1 << 31) - 1) / (4 * wmax) - 32) / kRowPad * kRowPad;
+    if ((size_t)M > cap) {
+        if (cap < (size_t)kRowPad || c_tp) return MM_E_ARG;
+        for (size_t m0 = 0; m0 < (size_t)M; m0 += cap) {
+            const int mr = (int)std::min(cap, (size_t)M - m0);
+            const size_t rt0 = m0 / 16;
+            const int rc = gemm_nt_f32a(prec, a + m0 * lda, lda, ascale, b_tp, mr, N, K, bias, relu,
+                                        mask ? mask + m0 * ldm : nullptr, ldm,
+                                        mbits_in ? mbits_in + rt0 * 64 * kMaskWords : nullptr,
+                                        mbits_out ? mbits_out + rt0 * 64 * kMaskWords : nullptr,
+                                        colsum ? colsum + rt0 * N : nullptr, cscale, c + m0 * ldc, ldc, nullptr, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale, c != nullptr};
     hipStream_t s = (hipStream_t)stream;
     BresPlan pl;
     int cfg = C_NARROW;

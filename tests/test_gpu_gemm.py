@@ -113,3 +113,29 @@ def test_gemm_rejects_bad_shapes():
         x3.gemm(a, x3.pack(torch.randn(264, 130, device="cuda")))
     with pytest.raises(_lib.MMError):  # x3 operands are exact splits: no scaling
         x3.gemm(torch.randn(100, 64, device="cuda"), x3.pack(torch.randn(8, 64, device="cuda")), ascale=2.0)
+
+
+@pytest.mark.parametrize("algo", ["auto", "stream"], indirect=True)
+def test_gemm_row_chunks(algo):
+    """A call whose A exceeds 2^31 bytes (the kernels address A and C through buffer resources) runs in
+    row chunks: 1,200,000 x 460 fp32 (2.2 GB), forward with bits and the input-gradient form, checked on
+    rows either side of the chunk boundary and at the end."""
+    M, N, K = 1_200_000, 264, 460
+    g = torch.Generator(device="cuda").manual_seed(11)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) * 0.05
+    b = torch.randn(N, device="cuda", generator=g)
+    bits = x3.mbits(M, "cuda")
+    y = x3.gemm(a, x3.pack(w), bias=b, relu=True, mbits_out=bits)
+    cap = ((2**31 - 1) // (4 * K) - 32) // 256 * 256
+    rows = torch.cat([torch.arange(0, 64), torch.arange(cap - 64, cap + 64), torch.arange(M - 64, M)]).cuda()
+    pre = a[rows].double() @ w.double().t() + b.double()
+    scale = a[rows].double().abs() @ w.double().abs().t() + b.double().abs()
+    assert _rel_err(y[rows], pre.clamp_min(0), scale) < TOL["x3"]
+    w2 = torch.randn(48, N, device="cuda", generator=g) * 0.1
+    dy = torch.randn(M, 48, device="cuda", generator=g)
+    cs = x3.colsum_buf(M, N, "cuda")
+    dx = x3.gemm(dy, x3.pack(w2, trans=True), mbits_in=bits, colsum=cs)
+    ref = (dy[rows].double() @ w2.double()) * (y[rows] > 0)
+    assert _rel_err(dx[rows], ref, dy[rows].double().abs() @ w2.double().abs()) < TOL["x3"]
+    assert torch.allclose(cs.double().sum(0), dx.double().sum(0), rtol=1e-5, atol=1e-3)
