@@ -86,7 +86,10 @@ struct ProjPtrs {  // the 23 Linear(d_i -> 20) modules' parameters (nn.Linear la
 __device__ __forceinline__ float4 xslice(const float* __restrict__ xr, int i, bool parity) {
     const int d = c_dims[i];
     const int s = parity ? 0 : c_starts_fixed[i];
-    return make_float4(xr[s], d > 1 ? xr[s + 1] : 0.f, d > 2 ? xr[s + 2] : 0.f, d > 3 ? xr[s + 3] : 0.f);
+    // four unconditional loads inside the slice (clamped index), zeros selected past d (no exec-masked
+    // loads)
+    const float v0 = xr[s], v1 = xr[s + min(1, d - 1)], v2 = xr[s + min(2, d - 1)], v3 = xr[s + min(3, d - 1)];
+    return make_float4(v0, d > 1 ? v1 : 0.f, d > 2 ? v2 : 0.f, d > 3 ? v3 : 0.f);
 }
 
 // o[r] = M[r] . xv + c[r] for the rows r of a [R][4] matrix (per-lane rows;
@@ -282,12 +285,15 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
             float o[kQkv];
             affine4<kQkv>(ti, ti + kQkv * kPin, xv, o);
 #pragma unroll
-            for (int a = 0; a < kKq; a++) {
-                q[a] = o[a];
-                Ks[g][i][a] = o[kKq + a];
-            }
+            for (int a = 0; a < kKq; a++) q[a] = o[a];
+            // 8- and 16-byte LDS writes (rows of 40 and 80 bytes) instead of 30 4-byte ones
 #pragma unroll
-            for (int c = 0; c < kEmb; c++) Vs[g][i][c] = o[2 * kKq + c];
+            for (int a = 0; a < kKq; a += 2)
+                *reinterpret_cast<float2*>(&Ks[g][i][a]) = make_float2(o[kKq + a], o[kKq + a + 1]);
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4)
+                *reinterpret_cast<float4*>(&Vs[g][i][c]) =
+                    make_float4(o[2 * kKq + c], o[2 * kKq + c + 1], o[2 * kKq + c + 2], o[2 * kKq + c + 3]);
         }
         wave_sync();
         if (act) {
