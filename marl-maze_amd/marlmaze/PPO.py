@@ -32,7 +32,7 @@ import random
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, x3
 from .dist import DP
 from .gemm_tuning import enable_tuned_gemms
 from .networks import Actor, Critic
@@ -189,6 +189,10 @@ class PPO:
         """Advance every maze ``horizon`` steps; fills the [T, N] buffers."""
         self._ensure_env()
         b, n, T = self._bufs, self.n_envs, self.horizon
+        with x3.cached_packs():  # the weights are fixed during the rollout: pack them once, not per step
+            return self._rollout_steps(b, n, T)
+
+    def _rollout_steps(self, b, n, T):
         head_w, head_b = self.actor.heads()
         for t in range(T):
             obs_t = b["obs"][t]

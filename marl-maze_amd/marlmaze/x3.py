@@ -4,6 +4,8 @@ A TP tensor is the int16 buffer holding an fp32 [R, C] matrix as three exact
 bf16 planes (precision "x3") or one fp16 plane ("f16") in MFMA fragment order
 (R padded to 256, C to 32).  ``TP`` carries its logical shape and precision.
 """
+import weakref
+
 import torch
 
 from . import _lib
@@ -25,15 +27,52 @@ class TP:
         return _lib.ptr(self.buf)
 
 
+# packed weights reused inside a ``cached_packs()`` scope (the rollout: the actor/critic weights are
+# fixed while it runs, and every step packs them): id(x) -> {(trans, prec, shape, stride): (weakref to
+# x, x._version, TP)}.  Opt-in, because not every in-place writer bumps the version counter (the fused
+# Adam step does not), so the cache lives only as long as the scope.
+_PACK_CACHE = {}
+_CACHE_ON = [False]
+
+
+class cached_packs:
+    """with x3.cached_packs(): ... -- pack() reuses the TP of an unchanged tensor within the scope."""
+
+    def __enter__(self):
+        _PACK_CACHE.clear()
+        _CACHE_ON[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _CACHE_ON[0] = False
+        _PACK_CACHE.clear()
+        return False
+
+
 def pack(x, out=None, trans=False, prec="x3"):
-    """fp32 [R, C] (or its transpose when trans=True, reading x as [C, R]) -> TP."""
+    """fp32 [R, C] (or its transpose when trans=True, reading x as [C, R]) -> TP (reused inside a
+    ``cached_packs()`` scope while the tensor is unchanged)."""
     assert x.dtype == torch.float32 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
     R, C = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
-    out = out if out is not None else TP(R, C, x.device, prec=prec)
-    assert (out.R, out.C, out.prec) == (R, C, prec)
-    _lib.check(_lib.lib().mm_gemm_tp_pack(PRECS[prec], _lib.ptr(x), R, C, x.stride(0), int(trans), out.ptr(),
+    key = (bool(trans), prec, tuple(x.shape), x.stride(0))
+    cache = out is None and _CACHE_ON[0]
+    if cache:
+        ent = _PACK_CACHE.get(id(x), {}).get(key)
+        if ent is not None and ent[0]() is x and ent[1] == x._version:
+            return ent[2]
+    res = out if out is not None else TP(R, C, x.device, prec=prec)
+    assert (res.R, res.C, res.prec) == (R, C, prec)
+    _lib.check(_lib.lib().mm_gemm_tp_pack(PRECS[prec], _lib.ptr(x), R, C, x.stride(0), int(trans), res.ptr(),
                                           _lib.stream_ptr()), "mm_gemm_tp_pack")
-    return out
+    if cache:
+        if len(_PACK_CACHE) > 256:  # drop entries of tensors that are gone
+            for k in [k for k, v in _PACK_CACHE.items() if all(e[0]() is None for e in v.values())]:
+                del _PACK_CACHE[k]
+        d = _PACK_CACHE.get(id(x))
+        if d is None or any(e[0]() is not x for e in d.values()):  # a new tensor at a reused id
+            d = _PACK_CACHE[id(x)] = {}
+        d[key] = (weakref.ref(x), x._version, res)
+    return res
 
 
 def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None, ascale=1.0, out=None):
