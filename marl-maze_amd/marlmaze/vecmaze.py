@@ -12,6 +12,7 @@ Memory per maze (10x10 reference maze, 19x19 layout): 361 B layout + 64 B agents
 + 32 B scalars + 2.5 KB RNG state (touched only at reset).
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -77,7 +78,7 @@ class VecMaze:
         self.done = torch.zeros(self.n, dtype=torch.uint8, device=d)
         # pre-generation (mm_env_pregen): each maze's next maze is generated ahead on a side stream,
         # so a reset is a copy (the serial backtracker leaves the step's critical path)
-        self.pregen = bool(pregen)
+        self.pregen = bool(pregen) and os.environ.get("MARLMAZE_PREGEN", "1") != "0"
         if self.pregen:
             self.next_layout = torch.ones((self.n, stride), dtype=torch.uint8, device=d)
             self.next_mazes = torch.zeros((self.n, 32), dtype=torch.uint8, device=d)
