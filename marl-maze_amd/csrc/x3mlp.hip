@@ -163,7 +163,10 @@ __global__ __launch_bounds__(256) void k_tp_pack(const float* __restrict__ X, in
     }
 }
 
-constexpr int kWaves = 16;
+#ifndef X3_WAVES
+#define X3_WAVES 16
+#endif
+constexpr int kWaves = X3_WAVES;  // the streaming kernel's waves per workgroup (one row tile each)
 constexpr int kThreads = 64 * kWaves;
 constexpr int kBM = 16 * kWaves;  // rows per workgroup: one row tile per wave
 static_assert(kBM <= kRowPad, "A row blocks must stay inside the TP row padding");
@@ -1557,6 +1560,8 @@ static bool bres_plan(int prec, int M, int N, int K, int lda, int ldc, bool bits
     if (ctb > cmax) return false;
     nblk = (tiles + ctb - 1) / ctb;
     if (nblk > 1 && ctb < 4) return false;  // A re-read per block: x3 at K = 460 (3 tiles) measured slower
+    // f16 at K = 460 (two blocks: A of 460 columns read twice): the streaming kernel measured 0.81x
+    if (prec == MM_PREC_F16 && nblk > 1 && K > 288) return false;
     if (nblk > kBresMaxBlk) return false;
     cfg = (prec == MM_PREC_F16 && ctb > BresCfg<C_NARROW>::CT) ? C_WIDE : C_NARROW;
     pl.nblk = nblk;
