@@ -322,6 +322,15 @@ int mm_actor_front_prep(const float* const* wproj, const float* const* bproj, co
                         const float* wv, float* ws, void* stream);
 int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h, void* stream);
 
+/* mm_actor_front_fwd with the kernel chosen by `algo` (bit-identical h):
+ * MM_FRONT_FWD_ROW1 (mm_actor_front_fwd's): one query row per lane;
+ * MM_FRONT_FWD_ROW2: two query rows per lane, each k_j / v_j LDS read feeding
+ * both (half the K/V LDS reads per sample). */
+#define MM_FRONT_FWD_ROW1 0
+#define MM_FRONT_FWD_ROW2 1
+int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, int B, int parity, float* h, int algo,
+                          void* stream);
+
 /* Backward of mm_actor_front_fwd for the upstream gradient dh [B, 460]: a
  * persistent grid of `grid` workgroups (2 per CU is the design point), each
  * writing one row of partial [grid, mm_actor_front_partial_len()]; the rows

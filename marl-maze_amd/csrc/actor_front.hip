@@ -92,6 +92,8 @@ __device__ __forceinline__ float4 xslice(const float* __restrict__ xr, int i, bo
     return make_float4(v0, d > 1 ? v1 : 0.f, d > 2 ? v2 : 0.f, d > 3 ? v3 : 0.f);
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
 // o[r] = M[r] . xv + c[r] for the rows r of a [R][4] matrix (per-lane rows;
 // M and c 16-byte aligned, R % 4 == 0)
 template <int R>
@@ -112,6 +114,37 @@ __device__ __forceinline__ void affine4(const float* __restrict__ M, const float
             acc = fmaf(w.w, xv.w, acc);
             o[4 * r4 + u] = acc + cc[u];
         }
+    }
+}
+
+// affine4 over a column-major (transposed) [4][R] matrix: rows r, r + 1 of each column are adjacent, so
+// every step is one packed FMA on aligned pairs (the [R][4] form needs two moves per packed FMA to pair
+// up rows).  Same per-element order as affine4 (mul, three fmas, + c): bit-identical results.
+template <int R>
+__device__ __forceinline__ void affine4t(const float* __restrict__ MT, const float* __restrict__ c, float4 xv,
+                                         float o[R]) {
+    const f32x2 x0 = {xv.x, xv.x}, x1 = {xv.y, xv.y}, x2 = {xv.z, xv.z}, x3 = {xv.w, xv.w};
+    const float4* m0 = reinterpret_cast<const float4*>(MT);
+    const float4* m1 = reinterpret_cast<const float4*>(MT + R);
+    const float4* m2 = reinterpret_cast<const float4*>(MT + 2 * R);
+    const float4* m3 = reinterpret_cast<const float4*>(MT + 3 * R);
+    const float4* c4 = reinterpret_cast<const float4*>(c);
+#pragma unroll
+    for (int r4 = 0; r4 < R / 4; r4++) {
+        const float4 a = m0[r4], b = m1[r4], d = m2[r4], e = m3[r4], cv = c4[r4];
+        f32x2 lo = f32x2{a.x, a.y} * x0, hi = f32x2{a.z, a.w} * x0;
+        lo = __builtin_elementwise_fma(f32x2{b.x, b.y}, x1, lo);
+        hi = __builtin_elementwise_fma(f32x2{b.z, b.w}, x1, hi);
+        lo = __builtin_elementwise_fma(f32x2{d.x, d.y}, x2, lo);
+        hi = __builtin_elementwise_fma(f32x2{d.z, d.w}, x2, hi);
+        lo = __builtin_elementwise_fma(f32x2{e.x, e.y}, x3, lo);
+        hi = __builtin_elementwise_fma(f32x2{e.z, e.w}, x3, hi);
+        lo = lo + f32x2{cv.x, cv.y};
+        hi = hi + f32x2{cv.z, cv.w};
+        o[4 * r4] = lo.x;
+        o[4 * r4 + 1] = lo.y;
+        o[4 * r4 + 2] = hi.x;
+        o[4 * r4 + 3] = hi.y;
     }
 }
 
@@ -138,7 +171,6 @@ __device__ __forceinline__ void wave_sync() {
 // (v_pk_fma_f32: two FMAs per instruction, half the dependent chain), summed at the end.  The
 // summation order is not the reference's (torch's CPU einsum order is not reproducible anyway; the
 // front-end is held to fp64 / torch within 1e-5).
-typedef __attribute__((ext_vector_type(2))) float f32x2;
 template <int N>
 __device__ __forceinline__ float dot4(const float* a, const float* __restrict__ b_lds) {  // N % 2 == 0
     f32x2 acc = {0.f, 0.f};
@@ -237,8 +269,9 @@ __global__ __launch_bounds__(256) void k_front_prep(ProjPtrs P, const float* __r
 // forward (persistent: the per-token tables are staged in LDS once per workgroup)
 // ---------------------------------------------------------------------------
 constexpr int kFwdRows = 8;  // samples per iteration of a 256-thread workgroup
-constexpr int kTabF = kQkv * kPin + kQkv + kEmb * kPin + kEmb;  // 300 floats per token: A | c | Wp | bp
-// (300 dwords = 75 16-byte quads, odd: a wave's per-token 16-byte reads are bank-conflict free)
+constexpr int kTabF = kQkv * kPin + kQkv + kEmb * kPin + kEmb;  // 300 floats per token: A^T | c | Wp^T | bp
+// (A and Wp column-major, [4][40] and [4][20], for affine4t; 300 dwords = 75 16-byte quads, odd: a wave's
+// per-token 16-byte reads are bank-conflict free)
 
 // all of a thread's table loads are issued before its LDS writes (one L2
 // round trip per workgroup instead of one per element); 256 threads
@@ -250,10 +283,12 @@ __device__ __forceinline__ void stage_tables(const float* __restrict__ ws, float
         const int e = threadIdx.x + 256 * u;
         const int i = e / kTabF, f = e % kTabF;
         int src;
-        if (f < kQkv * kPin) src = kWsA + i * kQkv * kPin + f;
+        if (f < kQkv * kPin) src = kWsA + i * kQkv * kPin + (f % kQkv) * kPin + f / kQkv;  // A^T[k][r] = A[r][k]
         else if (f < kQkv * kPin + kQkv) src = kWsC + i * kQkv + f - kQkv * kPin;
-        else if (f < kQkv * kPin + kQkv + kEmb * kPin) src = kWsWP + i * kEmb * kPin + f - kQkv * (kPin + 1);
-        else src = kWsBP + i * kEmb + f - kQkv * (kPin + 1) - kEmb * kPin;
+        else if (f < kQkv * kPin + kQkv + kEmb * kPin) {
+            const int g = f - kQkv * (kPin + 1);  // Wp^T[k][c] = Wp[c][k]
+            src = kWsWP + i * kEmb * kPin + (g % kEmb) * kPin + g / kEmb;
+        } else src = kWsBP + i * kEmb + f - kQkv * (kPin + 1) - kEmb * kPin;
         v[u] = e < kN ? ws[src] : 0.f;
     }
 #pragma unroll
@@ -283,7 +318,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
         float q[kKq];
         if (act) {
             float o[kQkv];
-            affine4<kQkv>(ti, ti + kQkv * kPin, xv, o);
+            affine4t<kQkv>(ti, ti + kQkv * kPin, xv, o);
 #pragma unroll
             for (int a = 0; a < kKq; a++) q[a] = o[a];
             // 8- and 16-byte LDS writes (rows of 40 and 80 bytes) instead of 30 4-byte ones
@@ -319,12 +354,143 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
 #pragma unroll
             for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] * inv, Vs[g][j]);
             float t[kEmb];
-            affine4<kEmb>(ti + kQkv * (kPin + 1), ti + kQkv * (kPin + 1) + kEmb * kPin, xv, t);
+            affine4t<kEmb>(ti + kQkv * (kPin + 1), ti + kQkv * (kPin + 1) + kEmb * kPin, xv, t);
             float* o = h + (size_t)row * kRowF + i * kEmb;
 #pragma unroll
             for (int c = 0; c < kEmb; c += 4)
                 *reinterpret_cast<float4*>(o + c) =
                     make_float4(t[c] + out[c], t[c + 1] + out[c + 1], t[c + 2] + out[c + 2], t[c + 3] + out[c + 3]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// forward, two query rows per lane (k_front_fwd2)
+// ---------------------------------------------------------------------------
+// k_front_fwd is bound by LDS data return, not by the VALU: every lane reads
+// all 23 k_j / v_j rows (690 floats) for its one query row, and a broadcast
+// read costs the same return bandwidth as a gather.  Here 16 lanes own a
+// sample and lane l owns query rows l and l + 12 (lane 11: row 11 only), so
+// each k_j / v_j read feeds two rows: per sample 12 x 690 instead of
+// 23 x 690 floats of K/V reads (the per-token table reads, 300 floats per
+// token, are unchanged).  Same arithmetic per row as k_front_fwd (dot4 /
+// axpy4 order, even/odd softmax sums), so h is bit-identical to it.
+constexpr int kF2Lanes = 16;                // lanes per sample
+constexpr int kF2Half = 12;                 // lane l owns rows l and l + 12
+constexpr int kF2Rows = 256 / kF2Lanes;     // 16 samples per workgroup iteration
+
+__global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__ ws, const float* __restrict__ x,
+                                                       int ldx, int B, int parity, float* __restrict__ h) {
+    __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
+    __shared__ __attribute__((aligned(16))) float Ks[kF2Rows][kTok][kKq];
+    __shared__ __attribute__((aligned(16))) float Vs[kF2Rows][kTok][kEmb];
+    stage_tables(ws, tab);
+    __syncthreads();
+    const int g = threadIdx.x >> 4;  // sample slot in the workgroup
+    const int l = threadIdx.x & 15;
+    const bool own0 = l < kF2Half, own1 = l + kF2Half < kTok;
+    const int i0 = own0 ? l : 0, i1 = own1 ? l + kF2Half : 0;  // rows (clamped: lane 11's second row is a
+                                                              // discarded copy of row 0)
+    const float* ta = tab + i0 * kTabF;
+    const float* tb = tab + i1 * kTabF;
+    const int groups = (B + kF2Rows - 1) / kF2Rows;
+    for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+        const int row = grp * kF2Rows + g;
+        const bool act = own0 && (row < B);
+        float4 xa = make_float4(0.f, 0.f, 0.f, 0.f), xb = xa;
+        if (act) {
+            const float* xr = x + (size_t)row * ldx;
+            xa = xslice(xr, i0, parity != 0);
+            xb = xslice(xr, i1, parity != 0);
+        }
+        wave_sync();  // previous iteration's K, V readers (this wavefront) are done
+        float qa[kKq], qb[kKq];
+        if (act) {
+            float o[kQkv];
+            affine4t<kQkv>(ta, ta + kQkv * kPin, xa, o);
+#pragma unroll
+            for (int a = 0; a < kKq; a++) qa[a] = o[a];
+#pragma unroll
+            for (int a = 0; a < kKq; a += 2)
+                *reinterpret_cast<float2*>(&Ks[g][i0][a]) = make_float2(o[kKq + a], o[kKq + a + 1]);
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4)
+                *reinterpret_cast<float4*>(&Vs[g][i0][c]) =
+                    make_float4(o[2 * kKq + c], o[2 * kKq + c + 1], o[2 * kKq + c + 2], o[2 * kKq + c + 3]);
+            affine4t<kQkv>(tb, tb + kQkv * kPin, xb, o);
+#pragma unroll
+            for (int a = 0; a < kKq; a++) qb[a] = o[a];
+            if (own1) {
+#pragma unroll
+                for (int a = 0; a < kKq; a += 2)
+                    *reinterpret_cast<float2*>(&Ks[g][i1][a]) = make_float2(o[kKq + a], o[kKq + a + 1]);
+#pragma unroll
+                for (int c = 0; c < kEmb; c += 4)
+                    *reinterpret_cast<float4*>(&Vs[g][i1][c]) =
+                        make_float4(o[2 * kKq + c], o[2 * kKq + c + 1], o[2 * kKq + c + 2], o[2 * kKq + c + 3]);
+            }
+        }
+        wave_sync();
+        if (act) {
+            float sa[kTok], sb[kTok];
+            float mxa = -INFINITY, mxb = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                sa[j] = div_sqrt_kq(dot4<kKq>(qa, Ks[g][j]));
+                sb[j] = div_sqrt_kq(dot4<kKq>(qb, Ks[g][j]));
+                mxa = fmaxf(mxa, sa[j]);
+                mxb = fmaxf(mxb, sb[j]);
+            }
+            float suma0 = 0.f, suma1 = 0.f, sumb0 = 0.f, sumb1 = 0.f;
+#pragma unroll
+            for (int j = 0; j < kTok; j++) {
+                sa[j] = expf(sa[j] - mxa);
+                sb[j] = expf(sb[j] - mxb);
+                if (j & 1) {
+                    suma1 += sa[j];
+                    sumb1 += sb[j];
+                } else {
+                    suma0 += sa[j];
+                    sumb0 += sb[j];
+                }
+            }
+            const float inva = 1.f / (suma0 + suma1), invb = 1.f / (sumb0 + sumb1);
+            float oa[kEmb], ob[kEmb];
+#pragma unroll
+            for (int c = 0; c < kEmb; c++) oa[c] = ob[c] = 0.f;
+            // partly unrolled: fully unrolled, the compiler hoists all 23 v_j reads (460 registers) and spills;
+            // sa / sb are then indexed by the wave-uniform j (register-relative moves, no scratch)
+#pragma unroll 4
+            for (int j = 0; j < kTok; j++) {  // one v_j read, two rows
+                const float4* v4 = reinterpret_cast<const float4*>(Vs[g][j]);
+                const float pa = sa[j] * inva, pb = sb[j] * invb;
+#pragma unroll
+                for (int k = 0; k < kEmb / 4; k++) {
+                    const float4 v = v4[k];
+                    oa[4 * k] = fmaf(pa, v.x, oa[4 * k]);
+                    oa[4 * k + 1] = fmaf(pa, v.y, oa[4 * k + 1]);
+                    oa[4 * k + 2] = fmaf(pa, v.z, oa[4 * k + 2]);
+                    oa[4 * k + 3] = fmaf(pa, v.w, oa[4 * k + 3]);
+                    ob[4 * k] = fmaf(pb, v.x, ob[4 * k]);
+                    ob[4 * k + 1] = fmaf(pb, v.y, ob[4 * k + 1]);
+                    ob[4 * k + 2] = fmaf(pb, v.z, ob[4 * k + 2]);
+                    ob[4 * k + 3] = fmaf(pb, v.w, ob[4 * k + 3]);
+                }
+            }
+            float t[kEmb];
+            float* hr = h + (size_t)row * kRowF;
+            affine4t<kEmb>(ta + kQkv * (kPin + 1), ta + kQkv * (kPin + 1) + kEmb * kPin, xa, t);
+#pragma unroll
+            for (int c = 0; c < kEmb; c += 4)
+                *reinterpret_cast<float4*>(hr + i0 * kEmb + c) =
+                    make_float4(t[c] + oa[c], t[c + 1] + oa[c + 1], t[c + 2] + oa[c + 2], t[c + 3] + oa[c + 3]);
+            if (own1) {
+                affine4t<kEmb>(tb + kQkv * (kPin + 1), tb + kQkv * (kPin + 1) + kEmb * kPin, xb, t);
+#pragma unroll
+                for (int c = 0; c < kEmb; c += 4)
+                    *reinterpret_cast<float4*>(hr + i1 * kEmb + c) =
+                        make_float4(t[c] + ob[c], t[c + 1] + ob[c + 1], t[c + 2] + ob[c + 2], t[c + 3] + ob[c + 3]);
+            }
         }
     }
 }
@@ -956,14 +1122,26 @@ static int cu_count() {
     return cus[dev];
 }
 
+extern "C" int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, int B, int parity, float* h,
+                                     int algo, void* stream) {
+    if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM) return MM_E_ARG;
+    if (algo != MM_FRONT_FWD_ROW1 && algo != MM_FRONT_FWD_ROW2) return MM_E_ARG;
+    if (B == 0) return 0;
+    if (algo == MM_FRONT_FWD_ROW2) {
+        const int groups = (B + kF2Rows - 1) / kF2Rows;
+        const int grid = groups < 2 * cu_count() ? groups : 2 * cu_count();  // two workgroups per CU (72 KB LDS)
+        hipLaunchKernelGGL(k_front_fwd2, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
+    } else {
+        const int groups = (B + kFwdRows - 1) / kFwdRows;
+        const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();  // three workgroups per CU
+        hipLaunchKernelGGL(k_front_fwd, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
+    }
+    return (int)hipGetLastError();
+}
+
 extern "C" int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h,
                                   void* stream) {
-    if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM) return MM_E_ARG;
-    if (B == 0) return 0;
-    const int groups = (B + kFwdRows - 1) / kFwdRows;
-    const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();  // three workgroups per CU
-    hipLaunchKernelGGL(k_front_fwd, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
-    return (int)hipGetLastError();
+    return mm_actor_front_fwd_ex(ws, x, ldx, B, parity, h, MM_FRONT_FWD_ROW1, stream);
 }
 
 extern "C" int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,

@@ -35,7 +35,7 @@ AF_HAS_MARK = 64
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample",
-           "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd",
+           "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd", "mm_actor_front_fwd_ex",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd", "mm_actor_front_bwd_ex",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
@@ -44,6 +44,7 @@ EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
 
 PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
+FRONT_FWD = {"row1": 0, "row2": 1}  # MM_FRONT_FWD_*
 GEMM_ALGO = {"auto": 0, "stream": 1}  # MM_GEMM_*
 
 
@@ -139,6 +140,8 @@ def lib():
         L.mm_actor_front_prep.restype = i32
         L.mm_actor_front_fwd.argtypes = [P, P, i32, i32, i32, P, P]
         L.mm_actor_front_fwd.restype = i32
+        L.mm_actor_front_fwd_ex.argtypes = [P, P, i32, i32, i32, P, i32, P]
+        L.mm_actor_front_fwd_ex.restype = i32
         L.mm_actor_front_grad_len.restype = i32
         L.mm_actor_front_partial_len.restype = i32
         L.mm_actor_front_bwd.argtypes = [P, P, i32, i32, i32, P, P, i32, P, P, P]

@@ -82,6 +82,9 @@ _CUS = {}
 # the front-end backward's attention products: "valu" (fp32 FMA, the default) or "mfma" (bf16x3 MFMA tiles;
 # measured slower, csrc/actor_front.hip k_front_bwd_mfma)
 FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "valu")
+# the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads) or "row1" (one per lane);
+# bit-identical outputs (csrc/actor_front.hip k_front_fwd2 / k_front_fwd)
+FRONT_FWD_ALGO = _os.environ.get("MARLMAZE_FRONT_FWD", "row1")
 
 
 def _cu_count(dev):
@@ -116,8 +119,8 @@ class _FusedFront(torch.autograd.Function):
         _lib.check(L.mm_actor_front_prep(wp, bp, _lib.ptr(wq), _lib.ptr(wk), _lib.ptr(wv), _lib.ptr(ws), stream),
                    "mm_actor_front_prep")
         h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
-        _lib.check(L.mm_actor_front_fwd(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h), stream),
-                   "mm_actor_front_fwd")
+        _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
+                                           _lib.FRONT_FWD[FRONT_FWD_ALGO], stream), "mm_actor_front_fwd_ex")
         ctx.save_for_backward(x, ws)
         ctx.parity = parity
         return h

@@ -212,6 +212,44 @@ def test_fused_front_matches_torch(parity, algo, monkeypatch):
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-3 * b.abs().max().item())
 
 
+@pytest.mark.parametrize("B", [1, 15, 17, 3001, 131072])
+@pytest.mark.parametrize("parity", [True, False])
+def test_front_forward_row2_bit_identical(parity, B):
+    """k_front_fwd2 (two query rows per lane) writes the same bits as
+    k_front_fwd (one row per lane): same per-row arithmetic; ragged B (not a
+    multiple of the 16 samples per workgroup iteration) and the persistent
+    grid's multi-iteration case (131,072 rows)."""
+    import ctypes
+
+    from marlmaze import _lib
+    from marlmaze.networks import Actor, front_params
+
+    torch.manual_seed(2)
+    actor = Actor([264, 264, 264], parity_mode=parity).cuda()
+    with torch.no_grad():
+        for p in actor.parameters():
+            p.mul_(3.0)
+    x = torch.randn(B, 65, device="cuda")
+    params = front_params(actor.projection, actor.attention)
+    L = _lib.lib()
+    ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device="cuda")
+    ptrs = [p.data_ptr() for p in params]
+    wp = (ctypes.c_void_p * 23)(*ptrs[:23])
+    bp = (ctypes.c_void_p * 23)(*ptrs[23:46])
+    s = _lib.stream_ptr()
+    _lib.check(L.mm_actor_front_prep(wp, bp, ptrs[46], ptrs[47], ptrs[48], _lib.ptr(ws), s), "prep")
+    hs = []
+    for algo in ("row1", "row2"):
+        h = torch.full((B + 1, 460), float("nan"), device="cuda")  # one guard row past B
+        _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), 65, B, int(parity), _lib.ptr(h),
+                                           _lib.FRONT_FWD[algo], s), algo)
+        hs.append(h)
+    torch.cuda.synchronize()
+    assert torch.isfinite(hs[1][:B]).all()
+    assert torch.isnan(hs[1][B]).all()  # nothing written past B
+    assert torch.equal(hs[0][:B], hs[1][:B])
+
+
 @pytest.mark.parametrize("parity", [True, False])
 def test_front_backward_mfma_vs_fp64(parity, monkeypatch):
     """The front-end's parameter gradients against an fp64 evaluation of the

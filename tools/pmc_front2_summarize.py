@@ -2,8 +2,9 @@
 import collections
 import csv
 import glob
+import sys
 
-for d in sorted(glob.glob("gpurun_out/pmc_front2_p*")):
+for d in sorted(glob.glob(f"gpurun_out/pmc_front2{sys.argv[1] if len(sys.argv) > 1 else ''}_p*")):
     f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
     if not f:
         continue
