@@ -23,7 +23,7 @@
 // b_i, so dWqkv = sum_i (E_i Wp_i^T + e_i b_i^T) -- formed once in
 // k_front_combine (92k FMAs per call) instead of 18.4k FMAs per sample.
 //
-// Workspace (k_front_prep): [Wp 23x20x4 | bp 23x20 | A 23x40x4 | c 23x40 | Wqkv 40x20]
+// Workspace (k_front_prep): [Wp 23x20x4 | bp 23x20 | A 23x40x4 | c 23x40 | Wqkv 40x20 | A^T 23x4x40]
 // Forward : x [B, ldx] -> h [B, 460] = t + softmax(q k^T / sqrt(10)) v
 // Backward: persistent grid of 256-thread workgroups (8 samples per
 //           iteration, two workgroups per CU); fixed entry -> thread maps, so
@@ -61,7 +61,8 @@ constexpr int kWsBP = kWsWP + kTok * kEmb * kPin;  // [23][20]
 constexpr int kWsA = kWsBP + kTok * kEmb;          // [23][40][4]
 constexpr int kWsC = kWsA + kTok * kQkv * kPin;    // [23][40]
 constexpr int kWsW = kWsC + kTok * kQkv;           // [40][20]
-constexpr int kWsLen = kWsW + kQkv * kEmb;         // 7700
+constexpr int kWsAT = kWsW + kQkv * kEmb;          // [23][4][40]: A column-major (the forward's staged tables)
+constexpr int kWsLen = kWsAT + kTok * kPin * kQkv;  // 11380
 
 // backward partial row (floats)
 constexpr int kGd = kQkv + kEmb;                    // 60 rows per token: g (40) then dctx (20)
@@ -257,6 +258,7 @@ __global__ __launch_bounds__(256) void k_front_prep(ProjPtrs P, const float* __r
         float acc = 0.f;
         for (int c = 0; c < kEmb; c++) acc = fmaf(W[r][c], Wp[c][k], acc);
         ws[kWsA + i * kQkv * kPin + e] = acc;
+        ws[kWsAT + i * kQkv * kPin + k * kQkv + r] = acc;
     }
     for (int r = threadIdx.x; r < kQkv; r += blockDim.x) {  // c_i = Wqkv b_i
         float acc = 0.f;
@@ -283,7 +285,7 @@ __device__ __forceinline__ void stage_tables(const float* __restrict__ ws, float
         const int e = threadIdx.x + 256 * u;
         const int i = e / kTabF, f = e % kTabF;
         int src;
-        if (f < kQkv * kPin) src = kWsA + i * kQkv * kPin + (f % kQkv) * kPin + f / kQkv;  // A^T[k][r] = A[r][k]
+        if (f < kQkv * kPin) src = kWsAT + i * kQkv * kPin + f;  // A^T
         else if (f < kQkv * kPin + kQkv) src = kWsC + i * kQkv + f - kQkv * kPin;
         else if (f < kQkv * kPin + kQkv + kEmb * kPin) {
             const int g = f - kQkv * (kPin + 1);  // Wp^T[k][c] = Wp[c][k]
@@ -511,8 +513,16 @@ constexpr int kEFUnits = kTok * (kGd / 4);           // 345 (token, 4 rows of [g
 
 // phase 4b of the backward: E/F (+= [g|dctx] x^T) and e/f (+= [g|dctx]) per token over the iteration's
 // samples; thread t owns units t and t + 256 (token u / 15, rows 4 (u % 15) ..), fixed order
+// accumulators held as aligned pairs: E rows (cols 0-1, 2-3) and e (rows 0-1, 2-3), so every update is a
+// packed FMA / add with the g value broadcast by op_sel (no pairing moves); per element the same fmaf / add
+// order as the scalar form
+struct EFAcc {
+    f32x2 e[2][4][2];  // [unit][row a][column pair]
+    f32x2 s[2][2];     // [unit][row pair]
+};
+
 template <int kStride = kSampleF, int kG = kOffG, int kD = kOffD, int kX = kOffX>
-__device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, float (&ae)[2][4][4], float (&as)[2][4]) {
+__device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, EFAcc& acc) {
 #pragma unroll
     for (int u = 0; u < 2; u++) {
         const int unit = threadIdx.x + u * kBwdThreads;
@@ -524,31 +534,42 @@ __device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, float (
                 const float4 gv = *reinterpret_cast<const float4*>(sg + off);
                 const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
                 const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
+                const f32x2 x01 = {xq.x, xq.y}, x23 = {xq.z, xq.w};
 #pragma unroll
                 for (int a = 0; a < 4; a++) {
-                    ae[u][a][0] = fmaf(gr[a], xq.x, ae[u][a][0]);
-                    ae[u][a][1] = fmaf(gr[a], xq.y, ae[u][a][1]);
-                    ae[u][a][2] = fmaf(gr[a], xq.z, ae[u][a][2]);
-                    ae[u][a][3] = fmaf(gr[a], xq.w, ae[u][a][3]);
-                    as[u][a] += gr[a];
+                    const f32x2 ga = {gr[a], gr[a]};
+                    acc.e[u][a][0] = __builtin_elementwise_fma(ga, x01, acc.e[u][a][0]);
+                    acc.e[u][a][1] = __builtin_elementwise_fma(ga, x23, acc.e[u][a][1]);
                 }
+                acc.s[u][0] += f32x2{gv.x, gv.y};
+                acc.s[u][1] += f32x2{gv.z, gv.w};
             }
         }
     }
 }
 
-__device__ __forceinline__ void ef_write(float* partial, const float (&ae)[2][4][4], const float (&as)[2][4]) {
+__device__ __forceinline__ void ef_zero(EFAcc& acc) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+#pragma unroll
+        for (int a = 0; a < 4; a++) acc.e[u][a][0] = acc.e[u][a][1] = f32x2{0.f, 0.f};
+        acc.s[u][0] = acc.s[u][1] = f32x2{0.f, 0.f};
+    }
+}
+
+__device__ __forceinline__ void ef_write(float* partial, const EFAcc& acc) {
     float* out = partial + (size_t)blockIdx.x * kPartLen;
 #pragma unroll
     for (int u = 0; u < 2; u++) {
         const int unit = threadIdx.x + u * kBwdThreads;
         if (unit < kEFUnits) {
             const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
+            const float sv[4] = {acc.s[u][0].x, acc.s[u][0].y, acc.s[u][1].x, acc.s[u][1].y};
 #pragma unroll
             for (int a = 0; a < 4; a++) {
                 *reinterpret_cast<float4*>(out + kPEF + (tk * kGd + r0 + a) * kPin) =
-                    make_float4(ae[u][a][0], ae[u][a][1], ae[u][a][2], ae[u][a][3]);
-                out[kPef + tk * kGd + r0 + a] = as[u][a];
+                    make_float4(acc.e[u][a][0].x, acc.e[u][a][0].y, acc.e[u][a][1].x, acc.e[u][a][1].y);
+                out[kPef + tk * kGd + r0 + a] = sv[a];
             }
         }
     }
@@ -563,11 +584,8 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
     const int i = threadIdx.x & 31;
     float* my = sm + g * kSampleF;
     // E/F/e/f: thread t owns units t and t + 256 (token u / 15, rows 4 (u % 15) ..)
-    float ae[2][4][4], as[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; u++)
-#pragma unroll
-        for (int a = 0; a < 4; a++) ae[u][a][0] = ae[u][a][1] = ae[u][a][2] = ae[u][a][3] = as[u][a] = 0.f;
+    EFAcc ef;
+    ef_zero(ef);
     const int iters = (B + kBwdRows - 1) / kBwdRows;
     for (int it = blockIdx.x; it < iters; it += gridDim.x) {
         const int row0 = it * kBwdRows;
@@ -693,9 +711,9 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
             *reinterpret_cast<float4*>(my + kOffX + i * kPin) = xv;
         }
         __syncthreads();
-        ef_accumulate(sm, nrow, ae, as);
+        ef_accumulate(sm, nrow, ef);
     }
-    ef_write(partial, ae, as);
+    ef_write(partial, ef);
 }
 
 // ---------------------------------------------------------------------------
@@ -787,11 +805,8 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd_mfma(const float* 
         }
     }
     const int wave = threadIdx.x >> 6;
-    float ae[2][4][4], as[2][4];
-#pragma unroll
-    for (int u = 0; u < 2; u++)
-#pragma unroll
-        for (int a = 0; a < 4; a++) ae[u][a][0] = ae[u][a][1] = ae[u][a][2] = ae[u][a][3] = as[u][a] = 0.f;
+    EFAcc ef;
+    ef_zero(ef);
     const float* const fA = tA;  // folded maps [23][40][4] (LDS)
     const float* const fC = tC;  // [23][40]
     // output r (0-9 q, 10-19 k, 20-39 v) of token t for input slice xv; 0 for padding tokens
@@ -1033,9 +1048,9 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd_mfma(const float* 
                 *reinterpret_cast<float4*>(my + kMD + 4 * e) = *reinterpret_cast<const float4*>(dhr + 4 * e);
         }
         __syncthreads();
-        ef_accumulate<kMmaSample, kMG, kMD, kMX>(sm, nrow, ae, as);
+        ef_accumulate<kMmaSample, kMG, kMD, kMX>(sm, nrow, ef);
     }
-    ef_write(partial, ae, as);
+    ef_write(partial, ef);
 }
 
 // sum of the partial rows: workgroup = 64 columns x 16 row classes (r mod 16);
