@@ -31,6 +31,8 @@ AF_HAS_KEY = 8
 AF_SEES_KEY = 16
 AF_TEAM_KEY = 32
 AF_HAS_MARK = 64
+ST_GEN_FAIL = 1  # MM_ST_* (maze status word)
+ST_BAD_MOVE = 2
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",

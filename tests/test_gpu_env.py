@@ -247,3 +247,49 @@ def test_pregeneration_is_invisible(cfg):
     envs[1]._kick_pregen()
     torch.cuda.synchronize()
     assert (envs[1].gen_state.cpu() == 0).all()  # every maze's next maze is ready after one idle pass
+
+
+def test_illegal_move_is_refused_and_flagged():
+    """A move the action mask forbids (into a wall, or an out-of-range move
+    code) is refused and flagged with MM_ST_BAD_MOVE in the maze's status word;
+    the agent stays on its cell.  The reference walks into the wall after
+    printing (maze.py:140-145), i.e. its state is undefined from there on; only
+    a caller that ignores the masks reaches this.  Mazes given legal actions in
+    the same launch are unaffected: bit-exact with the oracle."""
+    from marlmaze import _lib
+
+    n = 512
+    cfg = dict(default_size=(10, 10), max_timestep=1200)
+    env = VecMaze(n, seeds=list(range(n)), **cfg)
+    obs, masks = env.reset()
+    m = masks.cpu().numpy().astype(bool)
+    ora = OracleEnv(n, seeds=np.arange(n, dtype=np.uint64), **cfg)
+    oo, om = ora.reset_all()
+    assert np.array_equal(obs.cpu().numpy(), oo) and np.array_equal(m, om)
+    before = env.agent_info()
+    act = np.zeros((n, 2, 2), np.int8)
+    act[:, :, 0] = 4  # stay
+    bad = np.zeros(n, bool)
+    for i in range(0, n, 2):
+        walls = np.nonzero(~m[i, 0, :4])[0]
+        if i % 4 == 0 and len(walls):
+            act[i, 0, 0] = walls[0]  # into a wall
+            bad[i] = True
+        elif i % 4 == 2:
+            act[i, 0, 0] = 7  # not a move code
+            bad[i] = True
+    assert bad.sum() > n // 8
+    env.step(torch.as_tensor(act).cuda(), auto_reset=False)
+    st = env.status()
+    assert np.array_equal((st & _lib.ST_BAD_MOVE) != 0, bad)
+    assert not (st & ~np.uint16(_lib.ST_BAD_MOVE)).any()
+    after = env.agent_info()
+    assert np.array_equal(after["x"][bad, 0], before["x"][bad, 0])
+    assert np.array_equal(after["y"][bad, 0], before["y"][bad, 0])
+    ok = ~bad
+    act_ok = act.copy()
+    act_ok[bad, 0, 0] = 4  # the oracle follows the reference (walks into walls): give it legal actions there
+    o2, m2, r2, d2 = ora.step_all(act_ok, auto_reset=False)
+    assert np.array_equal(env.obs.cpu().numpy()[ok], o2[ok])
+    assert np.array_equal(env.masks.cpu().numpy().astype(bool)[ok], m2[ok])
+    assert np.array_equal(env.reward.cpu().numpy()[ok], r2[ok])

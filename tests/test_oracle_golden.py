@@ -163,3 +163,32 @@ def test_checkpoint_logits(golden):
     assert np.array_equal(mv.numpy(), c["move_logits"]) and np.array_equal(mr.numpy(), c["mark_logits"])
     assert np.array_equal(v.numpy(), c["values"])
     assert c["adam_step"] == 2175  # 87 epochs x 25 minibatch steps
+
+
+def test_oracle_under_asan_ubsan(tmp_path):
+    """Host sanitizers over the C oracle: oracle/asan_driver.c (resets and
+    random legal play, 10x10 / 20x20 / 4x4 / random-size / 6x6 mazes with
+    auto-reset, ~200k env-steps) built with AddressSanitizer + UBSan, every
+    finding fatal.  (GPU sanitizers are not available on this pool; the device
+    code shares env_device.h's logic with no host build.)"""
+    import os
+    import shutil
+    import subprocess
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    exe = str(tmp_path / "asan_driver")
+    cmd = ["gcc", "-O1", "-g", "-fno-omit-frame-pointer", "-std=c11", "-fsanitize=address,undefined",
+           "-fno-sanitize-recover=all", "-o", exe, os.path.join(here, "maze_oracle.c"),
+           os.path.join(here, "asan_driver.c"), "-lm"]
+    b = subprocess.run(cmd, capture_output=True, text=True)
+    if b.returncode != 0 and "asan" in b.stderr.lower():
+        pytest.skip("sanitizer runtime not available: " + b.stderr[-200:])
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "asan_driver ok" in r.stdout
+    assert "runtime error" not in r.stderr
