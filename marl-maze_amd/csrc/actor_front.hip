@@ -38,6 +38,14 @@
 
 namespace mm {
 
+// loop-unroll build knobs of the backward (tools/front_variants.sh; the defaults are the measured best)
+#ifndef FRONT_P3_UNROLL
+#define FRONT_P3_UNROLL 4
+#endif
+#ifndef FRONT_EF_UNROLL
+#define FRONT_EF_UNROLL 2
+#endif
+
 constexpr int kTok = 23;            // FEATURE_AMOUNT
 constexpr int kEmb = 20;            // EMBEDDING_DIM
 constexpr int kKq = 10;             // kq_dim
@@ -529,6 +537,7 @@ __device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, EFAcc& 
         if (unit < kEFUnits) {
             const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
             const int off = r0 < kQkv ? kG + tk * kQkv + r0 : kD + tk * kEmb + (r0 - kQkv);
+#pragma unroll FRONT_EF_UNROLL
             for (int gg = 0; gg < nrow; gg++) {
                 const float* sg = sm + gg * kStride;
                 const float4 gv = *reinterpret_cast<const float4*>(sg + off);
@@ -678,7 +687,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
             for (int c = 0; c < kEmb; c++) dv[c] = 0.f;
 #pragma unroll
             for (int a = 0; a < kKq; a++) dk[a] = 0.f;
-#pragma unroll 4
+#pragma unroll FRONT_P3_UNROLL
             for (int j = 0; j < kTok; j++) {
                 const float pj = my[kOffP + j * kTok + i];
                 const float sj = my[kOffS + j * kTok + i];
