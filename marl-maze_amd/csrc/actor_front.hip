@@ -45,6 +45,9 @@ namespace mm {
 #ifndef FRONT_EF_UNROLL
 #define FRONT_EF_UNROLL 2
 #endif
+#ifndef FRONT_EF_ROWS
+#define FRONT_EF_ROWS 4
+#endif
 
 constexpr int kTok = 23;            // FEATURE_AMOUNT
 constexpr int kEmb = 20;            // EMBEDDING_DIM
@@ -517,41 +520,53 @@ constexpr int kBwdThreads = 256;
 constexpr int kOffK = 0, kOffQ = 230, kOffV = 460, kOffP = 920, kOffS = 1449;  // attention phase
 constexpr int kOffG = 0, kOffD = 1380, kOffX = 1840;  // reduction phase
 constexpr int kSampleF = 1980;  // floats per sample (>= 1978 and >= 1932; multiple of 4)
-constexpr int kEFUnits = kTok * (kGd / 4);           // 345 (token, 4 rows of [g|dctx])
+// E/F work units: (token, kEFR consecutive rows of [g|dctx]); kEFR = FRONT_EF_ROWS (4: 345 units, two per
+// thread for 89 of 256 threads; 2: 690 units, three per thread for 178 -- a shorter critical thread)
+constexpr int kEFR = FRONT_EF_ROWS;
+static_assert(kEFR == 2 || kEFR == 4, "FRONT_EF_ROWS is 2 or 4");
+constexpr int kEFPerTok = kGd / kEFR;                                    // units per token
+constexpr int kEFUnits = kTok * kEFPerTok;                               // 345 / 690
+constexpr int kEFU = (kEFUnits + kBwdThreads - 1) / kBwdThreads;         // units per thread (2 / 3)
 
 // phase 4b of the backward: E/F (+= [g|dctx] x^T) and e/f (+= [g|dctx]) per token over the iteration's
-// samples; thread t owns units t and t + 256 (token u / 15, rows 4 (u % 15) ..), fixed order
-// accumulators held as aligned pairs: E rows (cols 0-1, 2-3) and e (rows 0-1, 2-3), so every update is a
-// packed FMA / add with the g value broadcast by op_sel (no pairing moves); per element the same fmaf / add
-// order as the scalar form
+// samples; thread t owns units t, t + 256, ... (token u / kEFPerTok, rows kEFR (u % kEFPerTok) ..), fixed
+// order.  Accumulators held as aligned pairs: E rows (cols 0-1, 2-3) and e (row pairs), so every update is
+// a packed FMA / add with the g value broadcast by op_sel (no pairing moves); per element the same fmaf /
+// add order as the scalar form
 struct EFAcc {
-    f32x2 e[2][4][2];  // [unit][row a][column pair]
-    f32x2 s[2][2];     // [unit][row pair]
+    f32x2 e[kEFU][kEFR][2];  // [unit][row a][column pair]
+    f32x2 s[kEFU][kEFR / 2];  // [unit][row pair]
 };
 
 template <int kStride = kSampleF, int kG = kOffG, int kD = kOffD, int kX = kOffX>
 __device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, EFAcc& acc) {
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < kEFU; u++) {
         const int unit = threadIdx.x + u * kBwdThreads;
         if (unit < kEFUnits) {
-            const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
+            const int tk = unit / kEFPerTok, r0 = kEFR * (unit % kEFPerTok);
             const int off = r0 < kQkv ? kG + tk * kQkv + r0 : kD + tk * kEmb + (r0 - kQkv);
 #pragma unroll FRONT_EF_UNROLL
             for (int gg = 0; gg < nrow; gg++) {
                 const float* sg = sm + gg * kStride;
-                const float4 gv = *reinterpret_cast<const float4*>(sg + off);
+                float gr[kEFR];
+                if constexpr (kEFR == 4) {
+                    const float4 gv = *reinterpret_cast<const float4*>(sg + off);
+                    gr[0] = gv.x, gr[1] = gv.y, gr[2] = gv.z, gr[3] = gv.w;
+                } else {
+                    const float2 gv = *reinterpret_cast<const float2*>(sg + off);
+                    gr[0] = gv.x, gr[1] = gv.y;
+                }
                 const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
-                const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
                 const f32x2 x01 = {xq.x, xq.y}, x23 = {xq.z, xq.w};
 #pragma unroll
-                for (int a = 0; a < 4; a++) {
+                for (int a = 0; a < kEFR; a++) {
                     const f32x2 ga = {gr[a], gr[a]};
                     acc.e[u][a][0] = __builtin_elementwise_fma(ga, x01, acc.e[u][a][0]);
                     acc.e[u][a][1] = __builtin_elementwise_fma(ga, x23, acc.e[u][a][1]);
                 }
-                acc.s[u][0] += f32x2{gv.x, gv.y};
-                acc.s[u][1] += f32x2{gv.z, gv.w};
+#pragma unroll
+                for (int a = 0; a < kEFR / 2; a++) acc.s[u][a] += f32x2{gr[2 * a], gr[2 * a + 1]};
             }
         }
     }
@@ -559,26 +574,26 @@ __device__ __forceinline__ void ef_accumulate(const float* sm, int nrow, EFAcc& 
 
 __device__ __forceinline__ void ef_zero(EFAcc& acc) {
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < kEFU; u++) {
 #pragma unroll
-        for (int a = 0; a < 4; a++) acc.e[u][a][0] = acc.e[u][a][1] = f32x2{0.f, 0.f};
-        acc.s[u][0] = acc.s[u][1] = f32x2{0.f, 0.f};
+        for (int a = 0; a < kEFR; a++) acc.e[u][a][0] = acc.e[u][a][1] = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < kEFR / 2; a++) acc.s[u][a] = f32x2{0.f, 0.f};
     }
 }
 
 __device__ __forceinline__ void ef_write(float* partial, const EFAcc& acc) {
     float* out = partial + (size_t)blockIdx.x * kPartLen;
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
+    for (int u = 0; u < kEFU; u++) {
         const int unit = threadIdx.x + u * kBwdThreads;
         if (unit < kEFUnits) {
-            const int tk = unit / (kGd / 4), r0 = 4 * (unit % (kGd / 4));
-            const float sv[4] = {acc.s[u][0].x, acc.s[u][0].y, acc.s[u][1].x, acc.s[u][1].y};
+            const int tk = unit / kEFPerTok, r0 = kEFR * (unit % kEFPerTok);
 #pragma unroll
-            for (int a = 0; a < 4; a++) {
+            for (int a = 0; a < kEFR; a++) {
                 *reinterpret_cast<float4*>(out + kPEF + (tk * kGd + r0 + a) * kPin) =
                     make_float4(acc.e[u][a][0].x, acc.e[u][a][0].y, acc.e[u][a][1].x, acc.e[u][a][1].y);
-                out[kPef + tk * kGd + r0 + a] = sv[a];
+                out[kPef + tk * kGd + r0 + a] = (a & 1) ? acc.s[u][a / 2].y : acc.s[u][a / 2].x;
             }
         }
     }
@@ -592,7 +607,7 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
     const int g = threadIdx.x >> 5;
     const int i = threadIdx.x & 31;
     float* my = sm + g * kSampleF;
-    // E/F/e/f: thread t owns units t and t + 256 (token u / 15, rows 4 (u % 15) ..)
+    // E/F/e/f: thread t owns units t, t + 256, ... (ef_accumulate)
     EFAcc ef;
     ef_zero(ef);
     const int iters = (B + kBwdRows - 1) / kBwdRows;
