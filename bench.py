@@ -102,7 +102,6 @@ def main():
     ap.add_argument("--horizon", type=int, default=16, help="env-steps per maze per iteration")
     ap.add_argument("--max-t", type=int, default=1200, help="max_timestep (main.py:20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-tuned-gemms", action="store_true", help="library-default GEMM heuristics (gemm_tuning.py)")
     a = ap.parse_args()
 
     # MARLMAZE_DP_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
@@ -120,7 +119,7 @@ def main():
     samples_local = n * T
     batch_global = 5 * ((samples_local * world) // 5)
     agent = PPO(2, epochs=1, batch_size=batch_global, lr=1.4e-4, n_envs=n, horizon=T, load=False, verbose=False,
-                save=False, dp=dp, sample_seed=12345, tuned_gemms=not a.no_tuned_gemms, dtype=a.dtype,
+                save=False, dp=dp, sample_seed=12345, dtype=a.dtype,
                 env_config=dict(default_size=(a.size, a.size), max_timestep=a.max_t, seed_base=0))
 
     def iteration():

@@ -120,8 +120,15 @@ typedef struct {
     int32_t* gen_state;            /* [n] */
 } mm_env_t;
 
-/* Library version (major*100 + minor). */
+/* Library version (major*100 + minor).  The major number changes whenever a
+ * struct of this header changes (3: mm_env_t has its 19 fields). */
 int mm_version(void);
+
+/* sizeof(mm_env_t) as compiled into the library: a binding that mirrors the
+ * struct (ctypes, cffi, cgo) compares its own size with this before the first
+ * call -- mm_env_t is passed by pointer, so a short mirror would otherwise make
+ * the library read past the caller's struct. */
+int mm_env_desc_size(void);
 
 /* Bytes needed for layout_stride given the config (side_max^2). */
 int mm_layout_stride(int size_w, int size_h, int rand_sizes, int rand_lo, int rand_hi);
@@ -293,10 +300,51 @@ int mm_ppo_loss(const float* heads, const uint8_t* masks, const int8_t* actions,
 int mm_ppo_loss_bwd(const float* heads, const uint8_t* masks, const int8_t* actions, const float* coef,
                     const float* dloss, int M, float* dheads, void* stream);
 
-/* Split-K weight gradients (the Linear backward dW = dY^T X over >= 65,536
- * rows, networks.py:35-41 / :87-106 under autograd): out [n] = sum over s of
- * x [S, n] (s ascending) + addend [n] (addend may be NULL; out may alias it). */
-int mm_sum_leading(const float* x, int S, long n, const float* addend, float* out, void* stream);
+/* The rest of one update minibatch step (PPO.py:58-85; csrc/update_kernels.hip),
+ * so that the step is hand-written launches only.  Sums run in a fixed order.
+ *
+ * mm_colsum: out [N] = column sums of x [R, N] f32 -- the nn.Linear bias
+ * gradients (networks.py:35-41, 87-106 under autograd) from the GEMM engine's
+ * per-16-row-tile column sums.  Two passes: G slabs of rows into part [G, N]
+ * (caller-owned, G >= 1; NULL allowed when G == 1), then the G partials.
+ * mm_mse_loss: nn.MSELoss()(V, rtg) (PPO.py:78-80) for V, rtg [M] f32: partial
+ * [mm_mse_loss_partials(M)] per-workgroup sums of (V - rtg)^2 and (dv may be
+ * NULL) dv [M] = (V - rtg) * (2 / M), the loss's gradient.
+ * mm_losses_final: out[0] = -sum(ppo_partial) / M (the actor loss of
+ * mm_ppo_loss), out[1] = sum(mse_partial) / M (the critic loss). */
+int mm_colsum(const float* x, long R, int N, float* part, int G, float* out, void* stream);
+int mm_mse_loss_partials(int M);
+int mm_mse_loss(const float* v, const float* rtg, int M, float* dv, float* partial, void* stream);
+int mm_losses_final(const float* ppo_partial, int n_ppo, const float* mse_partial, int n_mse, int M, float* out,
+                    void* stream);
+
+/* clip_grad_norm_(params, max_norm) followed by Adam.step() (PPO.py:74-85),
+ * for up to 4 networks ("segments") at once, each over flat f32 buffers of n
+ * elements: param, grad, exp_avg, exp_avg_sq.  Per segment the gradient is
+ * first scaled, g0 = grad_scale * grad (1 / world after a data-parallel
+ * all-reduce of sums; 1.0 otherwise), the L2 norm of g0 (fp64 partial sums,
+ * fixed order) gives coef = min(1, max_norm / (norm + 1e-6)) (max_norm <= 0:
+ * no clipping), then torch.optim.Adam's rule on g = coef * g0: exp_avg += (1 - beta1) (g - exp_avg); exp_avg_sq = exp_avg_sq
+ * beta2 + (1 - beta2) g g; param += -step_size exp_avg / (sqrt(exp_avg_sq) /
+ * bc2_sqrt + eps), with step_size = lr / (1 - beta1^t) and bc2_sqrt =
+ * sqrt(1 - beta2^t) formed by the caller for step t.  grad is not modified.
+ * norms [nseg] (may be NULL) receives each segment's norm before clipping
+ * (clip_grad_norm_'s return value).  ws: mm_clip_adam_ws_len(nseg) floats,
+ * 8-byte aligned. */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    long n;
+    float max_norm;
+    float step_size;
+    float bc2_sqrt;
+    float grad_scale;
+} mm_adam_seg_t;
+long mm_clip_adam_ws_len(int nseg);
+int mm_clip_adam(const mm_adam_seg_t* segs, int nseg, float beta1, float beta2, float eps, float* ws, float* norms,
+                 void* stream);
 
 /* The actor's two heads fused with mm_sample: logits =
  * h W^T + b for the concatenated heads W = [move_head.weight; mark_head.weight]
@@ -352,6 +400,14 @@ int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int pari
 #define MM_FRONT_BWD_VALU 1
 int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
                           float* partial, int grid, float* red, float* grad, int algo, void* stream);
+/* mm_actor_front_bwd_ex writing each parameter gradient straight into its
+ * own buffer in the module's layout (the update's .grad storage): wproj_grad /
+ * bproj_grad are HOST arrays of the 23 device pointers of the gradients of
+ * projection.layers[i].weight [20, d_i] / .bias [20]; wq_grad, wk_grad [10, 20],
+ * wv_grad [20, 20]. */
+int mm_actor_front_bwd_to(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
+                          float* partial, int grid, float* red, float* const* wproj_grad, float* const* bproj_grad,
+                          float* wq_grad, float* wk_grad, float* wv_grad, int algo, void* stream);
 
 #ifdef __cplusplus
 }

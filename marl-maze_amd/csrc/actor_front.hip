@@ -1102,10 +1102,37 @@ __global__ __launch_bounds__(kSumCols * kSumClasses) void k_front_sum(const floa
 
 // parameter gradients: dWqkv = sum_i E_i Wp_i^T + e_i b_i^T; dWp_i = F_i + Wqkv^T E_i,
 // dbp_i = f_i + Wqkv^T e_i (fixed summation order)
+// destinations of the parameter gradients in the modules' own layouts (nn.Linear [out][in], [out]):
+// the update writes them straight into the .grad storage (no copies out of a packed buffer)
+struct FrontGradPtrs {
+    float* wq;
+    float* wk;
+    float* wv;
+    float* wp[kTok];  // [20][d_i]
+    float* bp[kTok];  // [20]
+};
+
+// SCATTER = false: the packed layout grad [kGradLen]; true: the per-parameter destinations dst
+template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_front_combine(const float* __restrict__ ws, const float* __restrict__ red,
-                                                       float* __restrict__ grad) {
+                                                       float* __restrict__ grad, FrontGradPtrs dst) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kGradLen) return;
+    auto put = [&](float v) {
+        if (!SCATTER) {
+            grad[e] = v;
+        } else if (e < kGP) {
+            const int r = e / kEmb, c = e % kEmb;
+            float* d = r < kKq ? dst.wq + r * kEmb : r < 2 * kKq ? dst.wk + (r - kKq) * kEmb : dst.wv + (r - 2 * kKq) * kEmb;
+            d[c] = v;
+        } else if (e < kGB) {
+            const int f = e - kGP, tk = f / (kEmb * kPin), c = (f / kPin) % kEmb, k = f % kPin;
+            if (k < c_dims[tk]) dst.wp[tk][c * c_dims[tk] + k] = v;
+        } else {
+            const int f = e - kGB;
+            dst.bp[f / kEmb][f % kEmb] = v;
+        }
+    };
     const float* W = ws + kWsW;  // [40][20]
     if (e < kGP) {
         const int r = e / kEmb, c = e % kEmb;
@@ -1117,17 +1144,17 @@ __global__ __launch_bounds__(256) void k_front_combine(const float* __restrict__
             for (int a = 0; a < kPin; a++) acc = fmaf(E[a], Wp[a], acc);
             acc = fmaf(red[kPef + tk * kGd + r], ws[kWsBP + tk * kEmb + c], acc);  // e_i[r] b_i[c]
         }
-        grad[e] = acc;
+        put(acc);
     } else if (e < kGB) {
         const int f = e - kGP, tk = f / (kEmb * kPin), c = (f / kPin) % kEmb, k = f % kPin;
         float acc = red[kPEF + (tk * kGd + kQkv + c) * kPin + k];  // F_i[c][k]
         for (int r = 0; r < kQkv; r++) acc = fmaf(W[r * kEmb + c], red[kPEF + (tk * kGd + r) * kPin + k], acc);
-        grad[e] = acc;
+        put(acc);
     } else {
         const int f = e - kGB, tk = f / kEmb, c = f % kEmb;
         float acc = red[kPef + tk * kGd + kQkv + c];  // f_i[c]
         for (int r = 0; r < kQkv; r++) acc = fmaf(W[r * kEmb + c], red[kPef + tk * kGd + r], acc);
-        grad[e] = acc;
+        put(acc);
     }
 }
 
@@ -1183,9 +1210,10 @@ extern "C" int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int 
     return mm_actor_front_fwd_ex(ws, x, ldx, B, parity, h, MM_FRONT_FWD_ROW1, stream);
 }
 
-extern "C" int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
-                                     float* partial, int grid, float* red, float* grad, int algo, void* stream) {
-    if (!ws || !x || !dh || !partial || !red || !grad || B < 0 || ldx < MM_OBS_DIM || grid <= 0) return MM_E_ARG;
+static int front_bwd(const float* ws, const float* x, int ldx, int B, int parity, const float* dh, float* partial,
+                     int grid, float* red, float* grad, const FrontGradPtrs* dst, int algo, void* stream) {
+    if (!ws || !x || !dh || !partial || !red || (!grad && !dst) || B < 0 || ldx < MM_OBS_DIM || grid <= 0)
+        return MM_E_ARG;
     if (algo != MM_FRONT_BWD_MFMA && algo != MM_FRONT_BWD_VALU) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
     if (algo == MM_FRONT_BWD_MFMA)
@@ -1198,8 +1226,35 @@ extern "C" int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, i
                        partial, grid, red);
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(k_front_combine, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, grad);
+    if (grad)
+        hipLaunchKernelGGL(k_front_combine<false>, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, grad,
+                           FrontGradPtrs{});
+    else
+        hipLaunchKernelGGL(k_front_combine<true>, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, nullptr, *dst);
     return (int)hipGetLastError();
+}
+
+extern "C" int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
+                                     float* partial, int grid, float* red, float* grad, int algo, void* stream) {
+    if (!grad) return MM_E_ARG;
+    return front_bwd(ws, x, ldx, B, parity, dh, partial, grid, red, grad, nullptr, algo, stream);
+}
+
+extern "C" int mm_actor_front_bwd_to(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
+                                     float* partial, int grid, float* red, float* const* wproj_grad,
+                                     float* const* bproj_grad, float* wq_grad, float* wk_grad, float* wv_grad,
+                                     int algo, void* stream) {
+    if (!wproj_grad || !bproj_grad || !wq_grad || !wk_grad || !wv_grad) return MM_E_ARG;
+    FrontGradPtrs d;
+    d.wq = wq_grad;
+    d.wk = wk_grad;
+    d.wv = wv_grad;
+    for (int i = 0; i < kTok; i++) {
+        if (!wproj_grad[i] || !bproj_grad[i]) return MM_E_ARG;
+        d.wp[i] = wproj_grad[i];
+        d.bp[i] = bproj_grad[i];
+    }
+    return front_bwd(ws, x, ldx, B, parity, dh, partial, grid, red, nullptr, &d, algo, stream);
 }
 
 extern "C" int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,

@@ -772,7 +772,9 @@ inline int check_env(const mm_env_t* env) {
 
 using namespace mm;
 
-extern "C" int mm_version(void) { return 100; }
+extern "C" int mm_version(void) { return 300; }
+
+extern "C" int mm_env_desc_size(void) { return (int)sizeof(mm_env_t); }
 
 extern "C" int mm_layout_stride(int size_w, int size_h, int rand_sizes, int rand_lo, int rand_hi) {
     const int side = rand_sizes ? 2 * rand_hi - 1 : 2 * (size_w > size_h ? size_w : size_h) - 1;

@@ -538,52 +538,3 @@ extern "C" int mm_ppo_loss_bwd(const float* heads, const uint8_t* masks, const i
                        actions, coef, dloss, M, dheads);
     return (int)hipGetLastError();
 }
-
-// ---------------------------------------------------------------------------
-// split-K partial sum (networks._split_k_wgrad): out[j] = sum_s x[s, j] (s in
-// order) + addend[j].  Replaces a torch reduction over the leading dim of the
-// [S, N*K] batched-GEMM partials plus the add of the remainder rows' GEMM.
-// ---------------------------------------------------------------------------
-namespace mm {
-__global__ __launch_bounds__(256) void k_sum_leading4(const float4* __restrict__ x, int S, long n4,
-                                                     const float4* __restrict__ addend, float4* __restrict__ out) {
-    for (long j = blockIdx.x * 256L + threadIdx.x; j < n4; j += (long)gridDim.x * 256) {
-        float4 a = x[j];
-        for (int s = 1; s < S; s++) {
-            const float4 b = x[(long)s * n4 + j];
-            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-        }
-        if (addend) {
-            const float4 b = addend[j];
-            a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-        }
-        out[j] = a;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_sum_leading1(const float* __restrict__ x, int S, long n,
-                                                     const float* __restrict__ addend, float* __restrict__ out) {
-    for (long j = blockIdx.x * 256L + threadIdx.x; j < n; j += (long)gridDim.x * 256) {
-        float a = x[j];
-        for (int s = 1; s < S; s++) a += x[(long)s * n + j];
-        if (addend) a += addend[j];
-        out[j] = a;
-    }
-}
-}  // namespace mm
-
-extern "C" int mm_sum_leading(const float* x, int S, long n, const float* addend, float* out, void* stream) {
-    if (!x || !out || S <= 0 || n <= 0) return MM_E_ARG;
-    const bool v4 = (n % 4 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)out % 16 == 0) &&
-                    (!addend || (uintptr_t)addend % 16 == 0);
-    const long units = v4 ? n / 4 : n;
-    const int grid = (int)((units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096);
-    if (v4)
-        hipLaunchKernelGGL(mm::k_sum_leading4, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                           reinterpret_cast<const float4*>(x), S, units, reinterpret_cast<const float4*>(addend),
-                           reinterpret_cast<float4*>(out));
-    else
-        hipLaunchKernelGGL(mm::k_sum_leading1, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, S, units, addend,
-                           out);
-    return (int)hipGetLastError();
-}

@@ -1494,6 +1494,14 @@ static int dispatch_nt(const AT* a, int lda, float ascale, const uint16_t* b_tp,
     else if (tiles <= 8) { NT = 8; ncb = 1; }
     else if (tiles <= 17) { NT = 17; ncb = 1; }
     else { NT = 15; ncb = (tiles + 14) / 15; }
+    // few rows (the rollout's 4,096-8,192-row calls, the reference's 3,000-sample minibatches): too few
+    // 256-row units to fill the chip, so the columns are split into 4-tile blocks (x5 workgroups at N =
+    // 264).  Needs the buffer-store epilogue when bits are involved (it writes whole mask bytes per block).
+    const int nrb = rup(M, kBM) / kBM;
+    if (tiles > 4 && !ep.ctp && (ep.bufok || (!ep.mbits_in && !ep.mbits_out)) && 2L * nrb * ncb <= persistent_grid()) {
+        NT = 4;
+        ncb = (tiles + 3) / 4;
+    }
     if (ncb * NT * 16 > rup(N, kRowPad)) return MM_E_ARG;  // B TP row padding would be overrun
     if (ep.ctp && ncb != 1) return MM_E_ARG;
     switch (NT) {

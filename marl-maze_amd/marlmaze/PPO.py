@@ -32,47 +32,63 @@ import random
 import numpy as np
 import torch
 
-from . import ops, x3
+from . import ops, update, x3
 from .dist import DP
-from .gemm_tuning import enable_tuned_gemms
 from .networks import Actor, Critic
 from .vecmaze import VecMaze
 
 MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
 
 
+def _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip):
+    """mm_ppo_loss: (coef [M] = d loss / d logp, per-workgroup partial sums of the surrogate)."""
+    from . import _lib
+
+    L = _lib.lib()
+    M = old_logp.shape[0]
+    old_logp, adv = old_logp.contiguous(), adv.contiguous()
+    coef = torch.empty(M, dtype=torch.float32, device=heads.device)
+    part = torch.empty(L.mm_ppo_loss_partials(M), dtype=torch.float32, device=heads.device)
+    _lib.check(L.mm_ppo_loss(_lib.ptr(heads), _lib.ptr(mk), _lib.ptr(a8), _lib.ptr(old_logp), _lib.ptr(adv), M,
+                             float(clip), _lib.ptr(coef), _lib.ptr(part), _lib.stream_ptr()), "mm_ppo_loss")
+    return coef, part
+
+
+def _ppo_loss_bwd(heads, mk, a8, coef, dloss):
+    """mm_ppo_loss_bwd: d loss / d heads [2M, 6] (dloss: a 1-element device tensor)."""
+    from . import _lib
+
+    dz = torch.empty_like(heads)
+    _lib.check(_lib.lib().mm_ppo_loss_bwd(_lib.ptr(heads), _lib.ptr(mk), _lib.ptr(a8), _lib.ptr(coef),
+                                          _lib.ptr(dloss), coef.shape[0], _lib.ptr(dz), _lib.stream_ptr()),
+               "mm_ppo_loss_bwd")
+    return dz
+
+
+def _u8(masks):
+    masks = masks.contiguous()
+    return masks.view(torch.uint8) if masks.dtype == torch.bool else masks.to(torch.uint8)
+
+
 class _PolicyLoss(torch.autograd.Function):
     """-mean(min(r A, clamp(r, 1-clip, 1+clip) A)), r = exp(logp - old_logp),
     logp = sum over the two agents of get_log_probs (PPO.py:62-72, 154-168),
-    straight from the [2M, 6] head logits (mm_ppo_loss, mm_ppo_loss_bwd)."""
+    straight from the [2M, 6] head logits (mm_ppo_loss, mm_ppo_loss_bwd), with
+    autograd (the update itself runs the kernels without it)."""
 
     @staticmethod
     def forward(ctx, heads, masks, act, old_logp, adv, clip):
-        from . import _lib
-
-        L = _lib.lib()
-        M = old_logp.shape[0]
         heads = heads.contiguous()
-        mk = masks.contiguous().view(torch.uint8) if masks.dtype == torch.bool else masks.to(torch.uint8).contiguous()
+        mk = _u8(masks)
         a8 = act.to(torch.int8).contiguous()
-        coef = torch.empty(M, dtype=torch.float32, device=heads.device)
-        part = torch.empty(L.mm_ppo_loss_partials(M), dtype=torch.float32, device=heads.device)
-        _lib.check(L.mm_ppo_loss(_lib.ptr(heads), _lib.ptr(mk), _lib.ptr(a8), _lib.ptr(old_logp.contiguous()),
-                                 _lib.ptr(adv.contiguous()), M, float(clip), _lib.ptr(coef), _lib.ptr(part),
-                                 _lib.stream_ptr()), "mm_ppo_loss")
+        coef, part = _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip)
         ctx.save_for_backward(heads, mk, a8, coef)
-        return -part.sum() / M
+        return -part.sum() / old_logp.shape[0]
 
     @staticmethod
     def backward(ctx, dloss):
-        from . import _lib
-
         heads, mk, a8, coef = ctx.saved_tensors
-        dz = torch.empty_like(heads)
-        dl = dloss.reshape(1).to(torch.float32).contiguous()
-        _lib.check(_lib.lib().mm_ppo_loss_bwd(_lib.ptr(heads), _lib.ptr(mk), _lib.ptr(a8), _lib.ptr(coef),
-                                              _lib.ptr(dl), coef.shape[0], _lib.ptr(dz), _lib.stream_ptr()),
-                   "mm_ppo_loss_bwd")
+        dz = _ppo_loss_bwd(heads, mk, a8, coef, dloss.reshape(1).to(torch.float32).contiguous())
         return dz, None, None, None, None, None
 
 
@@ -80,18 +96,13 @@ class PPO:
     def __init__(self, agent_amount, epochs=500, batch_size=15000, lr=0.0002, discount_rate=0.99, lam=0.95,
                  updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
                  seed=3234, sample_seed=None, device=None, model_path=MODEL_PATH, load=True, parity_mode=True,
-                 bootstrap=True, dp=None, verbose=True, save=True, tuned_gemms=True, episode_batches=False,
+                 bootstrap=True, dp=None, verbose=True, save=True, episode_batches=False,
                  episode_chunk=64, dtype="f32"):
         self.maze = None  # wired by Maze.__init__ (maze.py:39-42), as in the reference
         self.dp = dp if dp is not None else DP.single()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
-        if tuned_gemms and self.device.type == "cuda":
-            # pre-tuned library GEMM choice (gemm_tuning.py).  Process-wide side effect: TunableOp is
-            # switched on (lookup only, no tuning) for every later torch GEMM of this process, which
-            # then picks the recorded solution for shapes in the file; tuned_gemms=False leaves it off
-            enable_tuned_gemms()
         # networks are built on the CPU right after the seed, like PPO.py:7,16-17; only the CPU
         # generator is seeded (torch.manual_seed would also reset the caller's CUDA streams) and
         # its state is restored afterwards
@@ -106,11 +117,26 @@ class PPO:
         self.actor = Actor([264, 264, 264], parity_mode=parity_mode, gemm_prec=prec).to(self.device)
         self.critic = Critic(agent_amount, hidden_sizes=[64, 64], gemm_prec=prec).to(self.device)
         torch.random.set_rng_state(g)
-        self.dp.broadcast_params([self.actor, self.critic])
-        # Adam (PPO.py:18-19); on the GPU the fused multi-tensor kernel (same update rule, one launch)
-        fused = self.device.type == "cuda"
-        self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=lr, fused=fused)
-        self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=lr, fused=fused)
+        # Adam (PPO.py:18-19)
+        self.flat = None
+        if self.device.type == "cuda":
+            # both networks in one flat parameter buffer (marlmaze.update): the explicit backward writes
+            # into its gradient twin, one all-reduce under DP, clip + Adam for both in two launches
+            a = self.actor
+            order = [p for n, p in a.named_parameters() if not n.startswith(("move_head", "mark_head"))]
+            order += [a.move_head.weight, a.mark_head.weight, a.move_head.bias, a.mark_head.bias]
+            self.flat = update.FlatParams([order, list(self.critic.parameters())],
+                                          adjacent=[(a.move_head.weight, a.mark_head.weight),
+                                                    (a.move_head.bias, a.mark_head.bias)])
+            self.dp.broadcast_tensor(self.flat.data)
+            mom = (torch.zeros_like(self.flat.data), torch.zeros_like(self.flat.data))
+            self.actor_optim = update.FlatAdam(self.flat, 0, self.actor.parameters(), lr=lr, moments=mom)
+            self.critic_optim = update.FlatAdam(self.flat, 1, self.critic.parameters(), lr=lr, moments=mom)
+        else:  # the host (CPU torch) form, for CPU runs and tests
+            self.dp.broadcast_params([self.actor, self.critic])
+            self.actor_optim = torch.optim.Adam(self.actor.parameters(), lr=lr)
+            self.critic_optim = torch.optim.Adam(self.critic.parameters(), lr=lr)
+        self._one = torch.ones(1, dtype=torch.float32, device=self.device)  # d loss / d loss
 
         self.agent_amount = agent_amount
         self.epochs = epochs
@@ -350,32 +376,69 @@ class PPO:
         lp = (lp + torch.log(p)).view(M, 2)
         return lp[:, 0] + lp[:, 1]
 
-    def minibatch_grads(self, obs, act, old_logp, adv, rtg, masks):
+    def minibatch_grads(self, obs, act, old_logp, adv, rtg, masks, out=None):
         """Losses of PPO.py:62-80 and their gradients in every parameter's .grad
         (before the all-reduce, the clipping and Adam).  Returns (actor_loss,
-        critic_loss) as 0-dim tensors."""
-        V = self.critic(obs).view(-1)
+        critic_loss) as 0-dim tensors (views of ``out`` [2] when given).
+
+        On the GPU: no autograd.  The critic and actor forwards keep what their
+        backwards need; the policy loss (mm_ppo_loss) and the value loss
+        (mm_mse_loss) hand d loss / d logits and d loss / dV straight to the
+        explicit backwards (Actor / Critic .train_backward), which write into the
+        flat gradient buffer."""
+        if not obs.is_cuda:
+            return self._minibatch_grads_host(obs, act, old_logp, adv, rtg, masks)
         M = obs.shape[0]
-        if obs.is_cuda:  # PPO.py:62-72 as two kernels (mm_ppo_loss / _bwd) on the [2M, 6] head logits
-            heads = self.actor.logits(obs.reshape(2 * M, 65))
-            actor_loss = _PolicyLoss.apply(heads, masks.reshape(2 * M, 6), act.reshape(2 * M, 2), old_logp, adv,
-                                           self.clip)
-        else:
-            cur = self.policy_logp(obs, act, masks)
-            ratio = torch.exp(cur - old_logp)
-            s1 = ratio * adv
-            s2 = torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv
-            actor_loss = -torch.mean(torch.min(s1, s2))
+        a8 = (act if act.dtype == torch.int8 else act.to(torch.int8)).contiguous()
+        mk = _u8(masks)
+        V, csaved = self.critic.train_forward(obs.reshape(M, -1))
+        mse_part, dv = update.mse_loss(V, rtg)
+        heads, asaved = self.actor.train_forward(obs.reshape(2 * M, 65))
+        coef, ppo_part = _ppo_loss_fwd(heads, mk, a8, old_logp, adv, self.clip)
+        dz = _ppo_loss_bwd(heads, mk, a8, coef, self._one)
+        if out is None:
+            out = torch.empty(2, dtype=torch.float32, device=obs.device)
+        update.losses_final(ppo_part, mse_part, M, out)
+        self.actor.train_backward(asaved, dz)
+        self.critic.train_backward(csaved, dv)
+        return out[0], out[1]
+
+    def _minibatch_grads_host(self, obs, act, old_logp, adv, rtg, masks):
+        """The CPU torch form (autograd, the reference's formulas)."""
+        V = self.critic(obs).view(-1)
+        cur = self.policy_logp(obs, act, masks)
+        ratio = torch.exp(cur - old_logp)
+        s1 = ratio * adv
+        s2 = torch.clamp(ratio, 1 - self.clip, 1 + self.clip) * adv
+        actor_loss = -torch.mean(torch.min(s1, s2))
         critic_loss = torch.nn.functional.mse_loss(V, rtg)
-        self.actor_optim.zero_grad(set_to_none=True)  # backward assigns fresh gradients: no fill + add launches
+        self.actor_optim.zero_grad(set_to_none=True)
         self.critic_optim.zero_grad(set_to_none=True)
         (actor_loss + critic_loss).backward()  # disjoint parameters: same grads as two backwards
         return actor_loss.detach(), critic_loss.detach()
 
-    def minibatch_step(self, obs, act, old_logp, adv, rtg, masks):
+    def minibatch_step(self, obs, act, old_logp, adv, rtg, masks, out=None):
         """One iteration of PPO.py:58-85: losses, gradients, all-reduce (DP),
-        clip_grad_norm_ per network, Adam.  Returns (aloss, closs, gnorm_a, gnorm_c)."""
-        actor_loss, critic_loss = self.minibatch_grads(obs, act, old_logp, adv, rtg, masks)
+        clip_grad_norm_ per network, Adam.  Returns (aloss, closs, gnorm_a,
+        gnorm_c) as 0-dim tensors (views of ``out`` [4] when given).
+
+        On the GPU the step is the minibatch_grads launches, one all-reduce of the
+        flat gradient buffer under DP (sums; the 1 / world scale is folded into
+        the optimizer kernel), and mm_clip_adam for both networks."""
+        if self.flat is None:
+            return self._minibatch_step_host(obs, act, old_logp, adv, rtg, masks)
+        if out is None:
+            out = torch.empty(4, dtype=torch.float32, device=obs.device)
+        self.minibatch_grads(obs, act, old_logp, adv, rtg, masks, out=out[0:2])
+        scale = 1.0
+        if self.dp.active:
+            self.dp.allreduce_sum(self.flat.grad)
+            scale = 1.0 / self.dp.world
+        update.clip_adam([self.actor_optim, self.critic_optim], self.max_grad, norms=out[2:4], grad_scale=scale)
+        return out[0], out[1], out[2], out[3]
+
+    def _minibatch_step_host(self, obs, act, old_logp, adv, rtg, masks):
+        actor_loss, critic_loss = self._minibatch_grads_host(obs, act, old_logp, adv, rtg, masks)
         params = list(self.actor.parameters()) + list(self.critic.parameters())
         self.dp.allreduce_grads(params)
         gna = torch.nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad)
@@ -399,29 +462,37 @@ class PPO:
             index_list = torch.randperm(B, device=b_obs.device, generator=generator)
         else:
             index_list = torch.as_tensor(index_list, device=b_obs.device, dtype=torch.long)
-        # the reference's minibatch loop spans batch_size (Q8); a batch smaller than that (explicit
-        # horizon * n_envs < batch_size) is used whole instead of yielding empty minibatches
+        # the reference's minibatch loop spans batch_size (Q8).  Under DP, or for a batch smaller than
+        # batch_size (explicit horizon * n_envs < batch_size), the batch is used whole: exactly 5
+        # minibatches of local_bs // 5 (a remainder of < 5 samples is left out, as the reference's
+        # loop leaves out everything past batch_size)
         local_bs = min(self.batch_size // self.dp.world, B)
-        mb = local_bs // 5 if (self.dp.active or local_bs < self.batch_size) else self.mbatch_size
+        whole = self.dp.active or local_bs < self.batch_size
+        mb = local_bs // 5 if whole else self.mbatch_size
         if mb < 1:
             raise ValueError(f"batch of {B} samples per rank is too small for 5 minibatches")
+        starts = list(range(0, 5 * mb, mb)) if whole else list(range(0, local_bs, mb))
         # the reference shuffles once per batch (PPO.py:48-49): gather the batch into that order once,
         # so every minibatch is a contiguous slice (same rows, no per-minibatch gathers)
-        used = min(B, ((local_bs + mb - 1) // mb) * mb)
+        used = min(B, starts[-1] + mb)
         order = index_list[:used]
         p_obs, p_act, p_logp, p_advs, p_rtgs, p_masks = (t[order] for t in (b_obs, b_act, b_logp, b_advs, b_rtgs,
                                                                           b_masks))
         if p_obs.is_cuda:  # the fused policy-loss kernels take int8 actions and u8 masks: convert once
             p_act = p_act.to(torch.int8)
-            p_masks = p_masks.view(torch.uint8) if p_masks.dtype == torch.bool else p_masks.to(torch.uint8)
-        hist = []
+            p_masks = _u8(p_masks)
+        K = self.updates_per_batch * len(starts)
+        hist = torch.empty((K, 4), dtype=torch.float32, device=b_obs.device)
+        k = 0
         for _ in range(self.updates_per_batch):
             self.decay_lr()
-            for start in range(0, local_bs, mb):
+            for start in starts:
                 sl = slice(start, start + mb)
-                hist.append(torch.stack(self.minibatch_step(p_obs[sl], p_act[sl], p_logp[sl], p_advs[sl],
-                                                            p_rtgs[sl], p_masks[sl])))
-        hist = torch.stack(hist)
+                row = self.minibatch_step(p_obs[sl], p_act[sl], p_logp[sl], p_advs[sl], p_rtgs[sl], p_masks[sl],
+                                          **({"out": hist[k]} if self.flat is not None else {}))
+                if self.flat is None:
+                    hist[k] = torch.stack(row)
+                k += 1
         if self.dp.active:  # local losses -> global-minibatch losses (equal shards); norms are already global
             self.dp.allreduce_sum(hist)
             hist /= self.dp.world
@@ -513,19 +584,12 @@ class PPO:
                         "critic_optim": self.critic_optim.state_dict()}), self.model_path)
 
     def load_optim_state(self, opt, state):
-        """Adam.load_state_dict, keeping this build's Adam flavour: a state dict
-        written by the reference (CPU, fused=False) would otherwise switch the
-        GPU optimizer to the unfused path (the saved hyper-parameters replace the
-        group's).  The fused kernel keeps ``step`` as an fp32 device tensor."""
+        """Adam.load_state_dict, keeping this build's Adam: a state dict written
+        by the reference (CPU torch.optim.Adam) loads into the flat GPU optimizer
+        (marlmaze.update.FlatAdam) and back."""
         opt.load_state_dict(state)
-        fused = self.device.type == "cuda"
-        for group in opt.param_groups:
-            group["fused"] = fused or None
-            group["foreach"] = None
-            for p in group["params"]:
-                st = opt.state.get(p)
-                if st and "step" in st and fused:
-                    st["step"] = torch.as_tensor(st["step"], dtype=torch.float32, device=p.device).reshape(())
+        if self.flat is not None:
+            x3.invalidate_packs()
 
     def load_parameters(self):
         if os.path.exists(self.model_path):

@@ -19,7 +19,7 @@ RNG_WORDS = 625
 MAX_SIDE = 41
 MAZES_PER_BLOCK = 32
 
-ST_GEN_FAIL = 1
+ST_GEN_FAIL = 1  # MM_ST_* (maze status word)
 ST_BAD_MOVE = 2
 
 GAE_AUTO, GAE_COLUMN, GAE_WALK, GAE_SCAN = 0, 1, 2, 3  # mm_gae_ex algorithms
@@ -31,18 +31,19 @@ AF_HAS_KEY = 8
 AF_SEES_KEY = 16
 AF_TEAM_KEY = 32
 AF_HAS_MARK = 64
-ST_GEN_FAIL = 1  # MM_ST_* (maze status word)
-ST_BAD_MOVE = 2
 
 # exported symbols (tests check every one of them is present)
-EXPORTS = ("mm_version", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
+EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
            "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd", "mm_actor_front_fwd_ex",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd", "mm_actor_front_bwd_ex",
+           "mm_actor_front_bwd_to",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
-           "mm_sum_leading", "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
-           "mm_gemm_wgrad")
+           "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
+           "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
+           "mm_clip_adam_ws_len", "mm_clip_adam")
+VERSION = 300  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
@@ -62,6 +63,15 @@ class EnvDesc(ctypes.Structure):
         ("rng", ctypes.c_void_p), ("work", ctypes.c_void_p),
         ("next_layout", ctypes.c_void_p), ("next_mazes", ctypes.c_void_p), ("next_rng", ctypes.c_void_p),
         ("gen_state", ctypes.c_void_p),
+    ]
+
+
+class AdamSeg(ctypes.Structure):
+    """mirror of mm_adam_seg_t"""
+    _fields_ = [
+        ("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+        ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_long), ("max_norm", ctypes.c_float),
+        ("step_size", ctypes.c_float), ("bc2_sqrt", ctypes.c_float), ("grad_scale", ctypes.c_float),
     ]
 
 
@@ -120,8 +130,22 @@ def lib():
         L.mm_ppo_loss.restype = i32
         L.mm_ppo_loss_bwd.argtypes = [P, P, P, P, P, i32, P, P]
         L.mm_ppo_loss_bwd.restype = i32
-        L.mm_sum_leading.argtypes = [P, i32, ctypes.c_long, P, P, P]
-        L.mm_sum_leading.restype = i32
+        L.mm_colsum.argtypes = [P, ctypes.c_long, i32, P, i32, P, P]
+        L.mm_colsum.restype = i32
+        L.mm_mse_loss_partials.argtypes = [i32]
+        L.mm_mse_loss_partials.restype = i32
+        L.mm_mse_loss.argtypes = [P, P, i32, P, P, P]
+        L.mm_mse_loss.restype = i32
+        L.mm_losses_final.argtypes = [P, i32, P, i32, i32, P, P]
+        L.mm_losses_final.restype = i32
+        L.mm_clip_adam_ws_len.argtypes = [i32]
+        L.mm_clip_adam_ws_len.restype = ctypes.c_long
+        L.mm_clip_adam.argtypes = [ctypes.POINTER(AdamSeg), i32, f32, f32, f32, P, P, P]
+        L.mm_clip_adam.restype = i32
+        L.mm_actor_front_bwd_to.argtypes = [P, P, i32, i32, i32, P, P, i32, P, ctypes.POINTER(P), ctypes.POINTER(P),
+                                            P, P, P, i32, P]
+        L.mm_actor_front_bwd_to.restype = i32
+        L.mm_env_desc_size.restype = i32
         L.mm_gemm_tp_len.argtypes = [i32, i32, i32]
         L.mm_gemm_tp_len.restype = ctypes.c_long
         L.mm_gemm_tp_pack.argtypes = [i32, P, i32, i32, i32, i32, P, P]
@@ -150,6 +174,11 @@ def lib():
         L.mm_actor_front_bwd.restype = i32
         L.mm_actor_front_bwd_ex.argtypes = [P, P, i32, i32, i32, P, P, i32, P, P, i32, P]
         L.mm_actor_front_bwd_ex.restype = i32
+        # the structs this module mirrors must match the library's (a short mm_env_t mirror would make
+        # the library read past the caller's struct)
+        if L.mm_version() // 100 != VERSION // 100 or L.mm_env_desc_size() != ctypes.sizeof(EnvDesc):
+            raise MMError(f"{LIB_PATH}: ABI {L.mm_version()} / mm_env_t of {L.mm_env_desc_size()} bytes, "
+                          f"this binding expects {VERSION} / {ctypes.sizeof(EnvDesc)}: rebuild the library")
         _LIB = L
     return _LIB
 

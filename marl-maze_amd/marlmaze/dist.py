@@ -7,8 +7,10 @@ independent, so rollout and GAE need no communication; the exchange steps are
 1. advantage normalisation (PPO.py:47): one all-reduce of {sum A, sum A^2, n}
    in fp64, so mean and the unbiased std are global;
 2. one all-reduce of a single flat fp32 bucket holding every actor AND critic
-   gradient per minibatch step (278,383 params = 1.11 MB), averaged, before
-   clip_grad_norm_ so the clipped global norm is identical on every rank;
+   gradient per minibatch step (278,383 params = 1.11 MB) before clipping, so
+   the clipped global norm is identical on every rank.  On the GPU the bucket IS
+   the gradient storage (marlmaze.update.FlatParams: no gather or scatter) and
+   the 1 / world average is applied inside the optimizer kernel;
 3. per-epoch statistics (episodes finished, their lengths and shortest
    paths: three fp64 sums, ``episode_stats``).
 
@@ -68,6 +70,11 @@ class DP:
             for m in modules:
                 for p in m.parameters():
                     dist.broadcast(p.data, src=0)
+
+    def broadcast_tensor(self, t):
+        """Rank 0's t on every rank (the flat parameter buffer: one collective)."""
+        if self.active:
+            dist.broadcast(t, src=0)
 
     def allreduce_grads(self, params):
         """Average the gradients of ``params`` across ranks in ONE flat bucket."""

@@ -3,10 +3,12 @@
 Parameters keep the reference's module tree and ``state_dict`` names (so the
 shipped ``PPO.pth`` loads unchanged) and are created in the reference's order,
 so ``torch.manual_seed(s)`` gives the same initial weights.  ``forward`` does
-not replay the reference's 23 tiny Linear calls: the 23 feature embeddings are
-packed into ONE [460, k] GEMM, Q/K/V into ONE [20, 40] GEMM over all 23
-tokens, the two heads into ONE [264, 6] GEMM -- all fp32 GEMMs on the f32 MFMA
-path (hipBLASLt) -- with the same arithmetic per output element.
+not replay the reference's 23 tiny Linear calls: the projection, Q/K/V,
+attention and residual run as one fused HIP kernel (csrc/actor_front.hip),
+the MLP trunk, the two heads (as ONE [6, K] GEMM) and the critic on the
+hand-written MFMA GEMMs of csrc/x3mlp.hip, at every batch size.  The PPO
+update calls ``train_forward`` / ``train_backward``: an explicit backward
+that writes every gradient straight into the parameters' .grad storage.
 
 Quirk Q1 (networks.py:59-63): the reference never advances the slice index,
 so every embedding reads ``x[:, 0:d_i]`` and the actor sees only obs[0:4].
@@ -105,22 +107,8 @@ class _FusedFront(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, parity, *params):
-        from . import _lib
-
-        L = _lib.lib()
-        B = x.shape[0]
         x = x.contiguous()
-        ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device=x.device)
-        ptrs = [p.data_ptr() for p in params]
-        wp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
-        bp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[FEATURE_AMOUNT:2 * FEATURE_AMOUNT])
-        wq, wk, wv = params[2 * FEATURE_AMOUNT:]
-        stream = _lib.stream_ptr()
-        _lib.check(L.mm_actor_front_prep(wp, bp, _lib.ptr(wq), _lib.ptr(wk), _lib.ptr(wv), _lib.ptr(ws), stream),
-                   "mm_actor_front_prep")
-        h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
-        _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
-                                           _lib.FRONT_FWD[FRONT_FWD_ALGO], stream), "mm_actor_front_fwd_ex")
+        ws, h = _front_fwd(x, parity, params)
         ctx.save_for_backward(x, ws)
         ctx.parity = parity
         return h
@@ -161,39 +149,43 @@ def front_params(projection, attention):
 
 # The actor MLP (the 460 -> 264 -> 264 -> 264 ReLU trunk + the two heads,
 # networks.py:35-41) and the critic (130 -> 64 -> 64 -> 1, networks.py:87-102)
-# run on the hand-written GEMMs of csrc/x3mlp.hip, forward and backward:
+# run on the hand-written GEMMs of csrc/x3mlp.hip at every row count, forward
+# and backward:
 # * precision "x3" (default): fp32-class -- each operand split exactly into
 #   three bf16 parts, six bf16 MFMA products kept; "f16": one fp16 MFMA product
 #   per element (BASELINE configs[4]).  Storage, master weights and Adam stay
-#   fp32 in both.
-# * weights are packed once per call into fragment-order planes (tiny); the
+#   fp32 in both.  The actor heads always run at x3: the rollout's fused
+#   head + sampler kernel computes them in fp32, and the update's log-probs
+#   must be those of the same logits.
+# * weights are packed per call into fragment-order planes (tiny); the
 #   activations stay fp32 row-major and are converted inside the GEMMs;
 # * the forward GEMMs record their ReLU masks as bits; the input-gradient GEMMs
 #   apply them in their epilogue (no threshold_backward pass) and emit the
-#   per-tile column sums of the next layer's bias gradient;
+#   per-tile column sums of the next layer's bias gradient (summed by mm_colsum);
 # * weight gradients dW = dY^T X run on mm_gemm_wgrad (row-slice partials
 #   summed in a fixed order).
 # The fp16 backward GEMMs scale dY by 2^floor(log2 M): the losses are means
 # over M rows, so per-row gradients are ~1/M, and the scale keeps them in
 # fp16's normal range; the results are unscaled (powers of two: exact).
-# x3 below _X3_MIN_ROWS rows uses the fp32 library GEMMs instead (the same
-# accuracy class; small calls); MARLMAZE_GEMM=lib keeps every x3-precision
-# GEMM on the library.
-_X3_MIN_ROWS = 16384
+# Shapes the engine does not take (a non-ReLU activation, layers wider than
+# 272, inputs not a multiple of 4 wide) -- none of which the reference builds --
+# run as plain torch ops, with a warning on the GPU.
 GEMM_PRECISIONS = ("x3", "f16")
+_MAX_WIDTH = 272
+_WARNED = set()
 
 
-def _engine_ok(x, prec, widths):
-    if not x.is_cuda or x.dim() != 2 or x.stride(1) != 1 or any(n > 272 for n in widths):
-        return False
-    if prec == "x3":
-        return _os.environ.get("MARLMAZE_GEMM", "auto") != "lib" and x.shape[0] >= _X3_MIN_ROWS
-    return True  # f16: always (the library would compute in fp32)
+def _engine_ok(x, widths):
+    return x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and all(n <= _MAX_WIDTH for n in widths)
 
 
-def _x3_ok(x, layers):
-    """The actor trunk's x3 condition (kept for the tests and tools)."""
-    return _engine_ok(x, "x3", [lin.weight.shape[0] for lin in layers]) and x.shape[1] % 4 == 0
+def _warn_torch_path(what):
+    if what not in _WARNED:
+        _WARNED.add(what)
+        import warnings
+
+        warnings.warn(f"marlmaze: {what} is outside the hand-written GEMM engine's shapes; it runs as plain "
+                      "torch ops", RuntimeWarning, stacklevel=3)
 
 
 def _grad_scale(M, prec):
@@ -201,35 +193,11 @@ def _grad_scale(M, prec):
     return float(2.0 ** int(math.floor(math.log2(max(int(M), 1))))) if prec == "f16" else 1.0
 
 
-def _wgrad(dy, x, prec):
-    """dW = dY^T X (mm_gemm_wgrad on the GPU)."""
-    if not dy.is_cuda:
-        return dy.t().mm(x)
+def _wgrad(dy, x, prec, out=None):
+    """dW = dY^T X (mm_gemm_wgrad)."""
     from . import x3
 
-    return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=_grad_scale(dy.shape[0], prec))
-
-
-def _split_k_wgrad(dy, x):
-    """The library form of dW = dY^T X (hipBLASLt split-K batched GEMM + mm_sum_leading),
-    kept as the MARLMAZE_GEMM=lib path and for comparisons (tools/bench_wgrad.py)."""
-    M = x.shape[0]
-    S = 16 if M >= 16 * 4096 else 1
-    if S == 1:
-        return dy.t().mm(x)
-    m = M - M % S
-    part = torch.bmm(dy[:m].view(S, m // S, -1).transpose(1, 2), x[:m].view(S, m // S, -1))
-    rest = dy[m:].t().mm(x[m:]) if m < M else None
-    if not part.is_cuda:
-        return part.sum(0) if rest is None else part.sum(0) + rest
-    from . import _lib
-
-    # the S partials and the remainder rows' product summed in one pass (mm_sum_leading)
-    out = rest if rest is not None else torch.empty(part.shape[1:], dtype=part.dtype, device=part.device)
-    _lib.check(_lib.lib().mm_sum_leading(_lib.ptr(part), S, part[0].numel(),
-                                         _lib.ptr(rest) if rest is not None else None, _lib.ptr(out),
-                                         _lib.stream_ptr()), "mm_sum_leading")
-    return out
+    return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=_grad_scale(dy.shape[0], prec), out=out)
 
 
 def _mlp_fwd(h0, ws, bs, prec, need_bits):
@@ -248,13 +216,10 @@ def _mlp_fwd(h0, ws, bs, prec, need_bits):
     return hs, bits
 
 
-def _x3_trunk_fwd(h0, ws, bs, need_bits, prec="x3"):
-    return _mlp_fwd(h0, ws, bs, prec, need_bits)
-
-
-def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx):
+def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None):
     """Backward through the ReLU layers given dY of the last one (already through
     its ReLU) and that dY's per-tile column sums cs (None: sum dY itself).
+    outs: destinations [dW0, db0, dW1, db1, ...] (or None: allocated).
     Returns (dx or None, [dW0, db0, dW1, db1, ...])."""
     from . import x3
 
@@ -263,8 +228,9 @@ def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx):
     grads = [None] * (2 * L)
     dx = None
     for l in range(L - 1, -1, -1):
-        grads[2 * l] = _wgrad(dy, hs[l], prec)
-        grads[2 * l + 1] = dy.sum(0) if cs is None else cs.sum(0)
+        o_w, o_b = (outs[2 * l], outs[2 * l + 1]) if outs is not None else (None, None)
+        grads[2 * l] = _wgrad(dy, hs[l], prec, out=o_w)
+        grads[2 * l + 1] = x3.colsum(dy if cs is None else cs, out=o_b)
         wt = x3.pack(ws[l], trans=True, prec=prec)
         if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0): the ReLU bits of layer l-1's forward
             cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
@@ -274,9 +240,26 @@ def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx):
     return dx, grads
 
 
+def _heads_fwd(h, wh, bh):
+    """The heads (networks.py:38-41) at x3 precision (see above)."""
+    from . import x3
+
+    return x3.gemm(h, x3.pack(wh, prec="x3"), bias=bh)
+
+
+def _heads_bwd(dz, h, wh, bits, out_w=None, out_b=None):
+    """The heads' backward: (dY through the last ReLU, its tile column sums, dWh, dbh)."""
+    from . import x3
+
+    dwh = _wgrad(dz, h, "x3", out=out_w)
+    dbh = x3.colsum(dz, out=out_b)
+    dy, cs = x3.heads_bwd(dz, wh, bits)  # (dz Wh) * (h > 0), fp32
+    return dy, cs, dwh, dbh
+
+
 class _EngineTrunk(torch.autograd.Function):
-    """The actor trunk alone with autograd (Actor.trunk under grad; the update
-    uses _EngineActor).  apply(prec, h0, W0, b0, W1, b1, ...) -> h_last."""
+    """The actor trunk alone with autograd (Actor.trunk under grad).
+    apply(prec, h0, W0, b0, W1, b1, ...) -> h_last."""
 
     @staticmethod
     def forward(ctx, prec, h0, *params):
@@ -296,55 +279,28 @@ class _EngineTrunk(torch.autograd.Function):
 
 
 class _EngineActor(torch.autograd.Function):
-    """The actor MLP on the engine: trunk (networks.py:35-36) + heads (:38-41).
-    apply(prec, h0 [M, K0], Wh [J, K], bh [J], W0, b0, W1, b1, ...) -> logits [M, J].
-
-    Backward: the heads' gradient goes through the last ReLU in one kernel
-    (mm_x3_heads_bwd, using the last forward GEMM's ReLU bits); each
-    input-gradient GEMM applies the ReLU bits of the layer below in its
-    epilogue and emits per-tile column sums (that layer's bias gradient);
-    weight gradients on mm_gemm_wgrad."""
+    """The actor MLP on the engine with autograd: trunk (networks.py:35-36) +
+    heads (:38-41).  apply(prec, h0 [M, K0], Wh [J, K], bh [J], W0, b0, W1, b1,
+    ...) -> logits [M, J].  The update does not go through autograd
+    (Actor.train_forward / train_backward); this serves ``Actor`` under grad."""
 
     @staticmethod
     def forward(ctx, prec, h0, wh, bh, *params):
-        from . import x3
-
         ws, bs = params[0::2], params[1::2]
         hs, bits = _mlp_fwd(h0, ws, bs, prec, True)
-        z = x3.gemm(hs[-1], x3.pack(wh, prec=prec), bias=bh)
+        z = _heads_fwd(hs[-1], wh, bh)
         ctx.save_for_backward(*hs, wh, *ws)
         ctx.bits, ctx.prec = bits, prec
         return z
 
     @staticmethod
     def backward(ctx, dz):
-        from . import x3
-
         L = len(ctx.bits)
         saved = ctx.saved_tensors
         hs, wh, ws = saved[:L + 1], saved[L + 1], saved[L + 2:]
-        dz = dz.contiguous()
-        dwh = _wgrad(dz, hs[L], ctx.prec)
-        dbh = dz.sum(0)
-        dy, cs = x3.heads_bwd(dz, wh, ctx.bits[L - 1])  # through the last ReLU (fp32)
+        dy, cs, dwh, dbh = _heads_bwd(dz.contiguous(), hs[L], wh, ctx.bits[L - 1])
         dx, grads = _mlp_bwd(ctx.bits, hs, ws, dy, cs, ctx.prec, ctx.needs_input_grad[1])
         return (None, dx, dwh, dbh, *grads)
-
-
-class _X3Trunk:
-    """_EngineTrunk at precision x3: apply(h0, W0, b0, ...)."""
-
-    @staticmethod
-    def apply(*args):
-        return _EngineTrunk.apply("x3", *args)
-
-
-class _X3Actor:
-    """_EngineActor at precision x3: apply(h0, Wh, bh, W0, b0, ...)."""
-
-    @staticmethod
-    def apply(*args):
-        return _EngineActor.apply("x3", *args)
 
 
 def _critic_fwd(x, params, prec, need_bits):
@@ -357,66 +313,44 @@ def _critic_fwd(x, params, prec, need_bits):
     return x3.gemm(hs[-1], x3.pack(w2, prec=prec), bias=b2), hs, bits
 
 
+def _critic_bwd(hs, bits, params, dv, prec, outs=None):
+    """The critic's parameter gradients for dV [M, 1]: the value head through the
+    last ReLU in one kernel (mm_x3_heads_bwd, J = 1), the input-gradient GEMM
+    through the first ReLU (bits + bias-gradient column sums), weight gradients
+    on mm_gemm_wgrad.  outs: destinations in parameter order (or None)."""
+    from . import x3
+
+    w0, _, w1, _, w2, _ = params
+    o = outs if outs is not None else [None] * 6
+    dw2 = _wgrad(dv, hs[2], prec, out=o[4])
+    db2 = x3.colsum(dv, out=o[5])
+    dy, cs = x3.heads_bwd(dv, w2, bits[1])  # (dV W2) * (h2 > 0)
+    _, grads = _mlp_bwd(bits, hs[:2], (w0, w1), dy, cs, prec, False, outs=o[:4] if outs is not None else None)
+    return grads + [dw2, db2]
+
+
 class _EngineCritic(torch.autograd.Function):
-    """The critic on the engine.  apply(prec, x [M, 130], W0, b0, W1, b1, W2, b2)
-    -> V [M, 1].  Backward: the value head through the last ReLU in one kernel
-    (mm_x3_heads_bwd, J = 1), the input-gradient GEMM through the first ReLU
-    (bits + bias-gradient column sums), weight gradients on mm_gemm_wgrad; no
-    gradient for the observations."""
+    """The critic on the engine with autograd.  apply(prec, x [M, 130], W0, b0,
+    W1, b1, W2, b2) -> V [M, 1]; no gradient for the observations."""
 
     @staticmethod
     def forward(ctx, prec, x, *params):
         v, hs, bits = _critic_fwd(x, params, prec, True)
-        ctx.save_for_backward(*hs, params[0], params[2], params[4])
+        ctx.save_for_backward(*hs, *params)
         ctx.bits, ctx.prec = bits, prec
         return v
 
     @staticmethod
     def backward(ctx, dv):
-        from . import x3
-
-        x, h1, h2, w0, w1, w2 = ctx.saved_tensors
-        dv = dv.contiguous()
-        dw2 = _wgrad(dv, h2, ctx.prec)
-        db2 = dv.sum(0)
-        dy, cs = x3.heads_bwd(dv, w2, ctx.bits[1])  # (dV W2) * (h2 > 0)
-        _, grads = _mlp_bwd(ctx.bits, (x, h1), (w0, w1), dy, cs, ctx.prec, False)
-        return (None, None, *grads, dw2, db2)
+        saved = ctx.saved_tensors
+        return (None, None, *_critic_bwd(saved[:3], ctx.bits, saved[3:], dv.contiguous(), ctx.prec))
 
 
-def _linear_fwd(x, w, b, relu):
-    """y = x W^T + b (then ReLU), the ReLU in the GEMM epilogue on the GPU."""
-    if relu and x.is_cuda and x.dim() == 2:
-        return torch._addmm_activation(b, x, w.t())
-    y = F.linear(x, w, b)
-    return F.relu(y) if relu else y
-
-
-class _SplitKLinear(torch.autograd.Function):
-    """nn.Linear (optionally followed by ReLU) on the library GEMMs, with the
-    weight gradient dW = dY^T X as a split-K batched GEMM (_split_k_wgrad).  With
-    relu=True the forward applies bias + ReLU in the GEMM epilogue and the
-    backward masks dY by y > 0 (threshold_backward)."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, relu):
-        y = _linear_fwd(x, w, b, relu)
-        ctx.relu = relu
-        ctx.save_for_backward(x, w, y if relu else None)
-        return y
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, w, y = ctx.saved_tensors
-        if ctx.relu:
-            dy = torch.ops.aten.threshold_backward(dy, y, 0)
-        return dy.mm(w), _split_k_wgrad(dy, x), dy.sum(0), None
-
-
-def _linear(x, w, b, relu=False):
-    if x.is_cuda and torch.is_grad_enabled() and (x.requires_grad or w.requires_grad):
-        return _SplitKLinear.apply(x, w, b, relu)
-    return _linear_fwd(x, w, b, relu)
+def _grad_of(p):
+    """p.grad, allocated if absent (the update writes every element)."""
+    if p.grad is None:
+        p.grad = torch.empty_like(p)
+    return p.grad
 
 
 class Actor(nn.Module):
@@ -446,29 +380,41 @@ class Actor(nn.Module):
             self.move_head.weight *= 0.01
             self.mark_head.weight *= 0.01
 
+    def _adjacent(self, a, b):
+        """[a; b] as one view when b's storage directly follows a's (the flat parameter
+        layout of marlmaze.update places the two heads so), else None."""
+        if (a.is_contiguous() and b.is_contiguous() and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+                and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()):
+            n = a.shape[1:] if a.dim() > 1 else ()
+            return torch.as_strided(a, (a.shape[0] + b.shape[0],) + tuple(n), a.stride(), a.storage_offset())
+        return None
+
     def heads(self):
-        """[move_head; mark_head] as one [6, K] weight and [6] bias."""
-        return (torch.cat([self.move_head.weight, self.mark_head.weight], 0),
-                torch.cat([self.move_head.bias, self.mark_head.bias], 0))
+        """[move_head; mark_head] as one [6, K] weight and [6] bias (views when the
+        parameters are laid out adjacently, else concatenated copies)."""
+        mw, kw, mb, kb = self.move_head.weight, self.mark_head.weight, self.move_head.bias, self.mark_head.bias
+        w, b = self._adjacent(mw, kw), self._adjacent(mb, kb)
+        return (w if w is not None else torch.cat([mw, kw], 0), b if b is not None else torch.cat([mb, kb], 0))
 
     def forward(self, x):
         heads = self.logits(x)
         return [heads[:, :5], heads[:, 5:6]]
+
+    def _mlp_params(self):
+        return [t for lin in self.layers for t in (lin.weight, lin.bias)]
 
     def logits(self, x):
         """[B, 6] = [5 move logits | mark logit] (both heads of networks.py:38-41)."""
         w, b = self.heads()
         h = self._front(x)
         if self._engine(h):
-            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            params = self._mlp_params()
             if torch.is_grad_enabled() and (h.requires_grad or any(p.requires_grad for p in params + [w, b])):
                 return _EngineActor.apply(self.gemm_prec, h, w, b, *params)  # trunk + heads, fused backward
-            from . import x3
-
             with torch.no_grad():
                 hs, _ = _mlp_fwd(h, params[0::2], params[1::2], self.gemm_prec, False)
-                return x3.gemm(hs[-1], x3.pack(w, prec=self.gemm_prec), bias=b)
-        return _linear(self._mlp(h), w, b)
+                return _heads_fwd(hs[-1], w, b)
+        return F.linear(self._mlp(h), w, b)
 
     def trunk(self, x):
         """Everything up to the last hidden layer (networks.py:31-36)."""
@@ -482,26 +428,103 @@ class Actor(nn.Module):
         return self.attention(self.projection(x))  # host reference path (CPU tests only)
 
     def _engine(self, h):
-        return (self.activation is nn.ReLU and _engine_ok(h, self.gemm_prec, [lin.weight.shape[0] for lin in self.layers])
-                and all(lin.weight.shape[1] % 4 == 0 for lin in self.layers))
+        ok = (self.activation is nn.ReLU and _engine_ok(h, [lin.weight.shape[0] for lin in self.layers])
+              and all(lin.weight.shape[1] % 4 == 0 for lin in self.layers))
+        if h.is_cuda and not ok:
+            _warn_torch_path("this Actor's MLP")
+        return ok
 
     def _mlp(self, h):
         """The hidden layers (networks.py:35-36)."""
         if self._engine(h):
-            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            params = self._mlp_params()
             if torch.is_grad_enabled() and (h.requires_grad or any(p.requires_grad for p in params)):
                 return _EngineTrunk.apply(self.gemm_prec, h, *params)
             with torch.no_grad():
                 hs, _ = _mlp_fwd(h, params[0::2], params[1::2], self.gemm_prec, False)
             return hs[-1]
-        if self.activation is nn.ReLU:
-            for lin in self.layers:
-                h = _linear(h, lin.weight, lin.bias, relu=True)
-        else:
-            act = self.activation()
-            for lin in self.layers:
-                h = act(_linear(h, lin.weight, lin.bias))
+        act = self.activation()
+        for lin in self.layers:
+            h = act(F.linear(h, lin.weight, lin.bias))
         return h
+
+    # ---- the update's explicit forward / backward (no autograd; GPU) ----
+    def train_forward(self, x):
+        """x [M, 65] f32 on the GPU -> (head logits z [M, 6], saved state for
+        train_backward).  The forward of get_log_probs' actor calls (PPO.py:66-68)."""
+        x = x.contiguous()
+        ws, h0 = _front_fwd(x, self.projection.parity_mode, front_params(self.projection, self.attention))
+        if not self._engine(h0):
+            raise ValueError("Actor.train_forward needs the GPU engine's shapes (ReLU, widths <= 272)")
+        params = self._mlp_params()
+        hs, bits = _mlp_fwd(h0, params[0::2], params[1::2], self.gemm_prec, True)
+        w, b = self.heads()
+        z = _heads_fwd(hs[-1], w, b)
+        return z, (x, ws, hs, bits)
+
+    def train_backward(self, saved, dz):
+        """Every parameter's gradient for d loss / d z (dz [M, 6]), written into
+        the parameters' .grad storage (allocated when absent)."""
+        x, ws, hs, bits = saved
+        L = len(self.layers)
+        w, _ = self.heads()
+        gw = self._adjacent(_grad_of(self.move_head.weight), _grad_of(self.mark_head.weight))
+        gb = self._adjacent(_grad_of(self.move_head.bias), _grad_of(self.mark_head.bias))
+        dy, cs, dwh, dbh = _heads_bwd(dz.contiguous(), hs[L], w, bits[L - 1], out_w=gw, out_b=gb)
+        if gw is None:
+            self.move_head.weight.grad.copy_(dwh[:5])
+            self.mark_head.weight.grad.copy_(dwh[5:])
+        if gb is None:
+            self.move_head.bias.grad.copy_(dbh[:5])
+            self.mark_head.bias.grad.copy_(dbh[5:])
+        params = self._mlp_params()
+        dh0, _ = _mlp_bwd(bits, hs, params[0::2], dy, cs, self.gemm_prec, True,
+                          outs=[_grad_of(p) for p in params])
+        _front_bwd_to(ws, x, self.projection.parity_mode, dh0,
+                      [_grad_of(p) for p in front_params(self.projection, self.attention)])
+
+
+def _front_fwd(x, parity, params):
+    """The fused front-end forward (no autograd): (workspace, h [B, 460])."""
+    from . import _lib
+
+    L = _lib.lib()
+    B = x.shape[0]
+    ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device=x.device)
+    ptrs = [p.data_ptr() for p in params]
+    wp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
+    bp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[FEATURE_AMOUNT:2 * FEATURE_AMOUNT])
+    wq, wk, wv = params[2 * FEATURE_AMOUNT:]
+    stream = _lib.stream_ptr()
+    _lib.check(L.mm_actor_front_prep(wp, bp, _lib.ptr(wq), _lib.ptr(wk), _lib.ptr(wv), _lib.ptr(ws), stream),
+               "mm_actor_front_prep")
+    h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
+    _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
+                                       _lib.FRONT_FWD[FRONT_FWD_ALGO], stream), "mm_actor_front_fwd_ex")
+    return ws, h
+
+
+def _front_bwd_to(ws, x, parity, dh, grads):
+    """The fused front-end backward writing the parameter gradients into ``grads``
+    (front_params order; each in its module layout) -- mm_actor_front_bwd_to."""
+    from . import _lib
+
+    L = _lib.lib()
+    B = x.shape[0]
+    dh = dh.contiguous()
+    grid = max(1, min(2 * _cu_count(x.device), (B + 7) // 8))  # two 8-sample workgroups per CU
+    plen = L.mm_actor_front_partial_len()
+    partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
+    red = torch.empty(plen, dtype=torch.float32, device=x.device)
+    assert all(g.is_contiguous() for g in grads)
+    ptrs = [g.data_ptr() for g in grads]
+    gw = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
+    gb = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[FEATURE_AMOUNT:2 * FEATURE_AMOUNT])
+    gq, gk, gv = grads[2 * FEATURE_AMOUNT:]
+    _lib.check(L.mm_actor_front_bwd_to(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(dh),
+                                       _lib.ptr(partial), grid, _lib.ptr(red), gw, gb, _lib.ptr(gq), _lib.ptr(gk),
+                                       _lib.ptr(gv), _lib.FRONT_BWD[FRONT_BWD_ALGO], _lib.stream_ptr()),
+               "mm_actor_front_bwd_to")
 
 
 class Critic(nn.Module):
@@ -525,21 +548,44 @@ class Critic(nn.Module):
         for layer in self.layers:
             nn.init.orthogonal_(layer.weight)
 
+    def _params(self):
+        return [t for lin in self.layers for t in (lin.weight, lin.bias)]
+
+    def _engine(self, x):
+        # the engine's critic: three layers, hidden widths <= 64 (the 8-byte-row A source of the [M, 130] input)
+        ok = (len(self.layers) == 3 and self.activation is nn.ReLU and x.shape[1] % 2 == 0
+              and all(lin.weight.shape[0] <= 64 for lin in self.layers)
+              and _engine_ok(x, [lin.weight.shape[0] for lin in self.layers]))
+        if x.is_cuda and not ok:
+            _warn_torch_path("this Critic")
+        return ok
+
     def forward(self, x):
         x = torch.as_tensor(x, dtype=torch.float32, device=self.layers[0].weight.device)
         x = x.reshape(-1, self.agent_amount * OBS_SPACE)
-        if (len(self.layers) == 3 and self.activation is nn.ReLU and x.shape[1] % 2 == 0
-                and all(lin.weight.shape[0] <= 64 for lin in self.layers)
-                and _engine_ok(x, self.gemm_prec, [lin.weight.shape[0] for lin in self.layers])):
+        if self._engine(x):
             x = x.contiguous()
-            params = [t for lin in self.layers for t in (lin.weight, lin.bias)]
+            params = self._params()
             if torch.is_grad_enabled() and any(p.requires_grad for p in params):
                 return _EngineCritic.apply(self.gemm_prec, x, *params)
             with torch.no_grad():
                 return _critic_fwd(x, params, self.gemm_prec, False)[0]
+        act = self.activation()
         for lin in self.layers[:-1]:
-            if self.activation is nn.ReLU:
-                x = _linear(x, lin.weight, lin.bias, relu=True)
-            else:
-                x = self.activation()(_linear(x, lin.weight, lin.bias))
-        return _linear(x, self.layers[-1].weight, self.layers[-1].bias)
+            x = act(F.linear(x, lin.weight, lin.bias))
+        return F.linear(x, self.layers[-1].weight, self.layers[-1].bias)
+
+    # ---- the update's explicit forward / backward (no autograd; GPU) ----
+    def train_forward(self, x):
+        """x [M, agents * 65] f32 on the GPU -> (V [M, 1], saved state)."""
+        x = x.reshape(-1, self.agent_amount * OBS_SPACE).contiguous()
+        assert x.is_cuda and self._engine(x)
+        v, hs, bits = _critic_fwd(x, self._params(), self.gemm_prec, True)
+        return v, (hs, bits)
+
+    def train_backward(self, saved, dv):
+        """Every parameter's gradient for d loss / d V (dv [M, 1]) into .grad."""
+        hs, bits = saved
+        params = self._params()
+        _critic_bwd(hs, bits, params, dv.reshape(-1, 1).contiguous(), self.gemm_prec,
+                    outs=[_grad_of(p) for p in params])

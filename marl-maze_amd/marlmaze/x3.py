@@ -29,23 +29,33 @@ class TP:
 
 # packed weights reused inside a ``cached_packs()`` scope (the rollout: the actor/critic weights are
 # fixed while it runs, and every step packs them): id(x) -> {(trans, prec, shape, stride): (weakref to
-# x, x._version, TP)}.  Opt-in, because not every in-place writer bumps the version counter (the fused
-# Adam step does not), so the cache lives only as long as the scope.
+# x, data_ptr, x._version, generation, TP)}.  An entry is stale when the tensor's version counter moved
+# (torch in-place ops) or the generation did: the hand-written optimizer (marlmaze.update) and parameter
+# loads call ``invalidate_packs()``, because they write parameters without touching the version counter.
 _PACK_CACHE = {}
-_CACHE_ON = [False]
+_CACHE_DEPTH = [0]
+_GENERATION = [0]
+
+
+def invalidate_packs():
+    """Parameters were written outside torch's version tracking: cached packs are stale."""
+    _GENERATION[0] += 1
 
 
 class cached_packs:
-    """with x3.cached_packs(): ... -- pack() reuses the TP of an unchanged tensor within the scope."""
+    """with x3.cached_packs(): ... -- pack() reuses the TP of an unchanged tensor within the scope
+    (scopes nest; the cache is dropped when the outermost one ends)."""
 
     def __enter__(self):
-        _PACK_CACHE.clear()
-        _CACHE_ON[0] = True
+        if _CACHE_DEPTH[0] == 0:
+            _PACK_CACHE.clear()
+        _CACHE_DEPTH[0] += 1
         return self
 
     def __exit__(self, *exc):
-        _CACHE_ON[0] = False
-        _PACK_CACHE.clear()
+        _CACHE_DEPTH[0] -= 1
+        if _CACHE_DEPTH[0] == 0:
+            _PACK_CACHE.clear()
         return False
 
 
@@ -55,11 +65,12 @@ def pack(x, out=None, trans=False, prec="x3"):
     assert x.dtype == torch.float32 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
     R, C = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
     key = (bool(trans), prec, tuple(x.shape), x.stride(0))
-    cache = out is None and _CACHE_ON[0]
+    cache = out is None and _CACHE_DEPTH[0] > 0
     if cache:
         ent = _PACK_CACHE.get(id(x), {}).get(key)
-        if ent is not None and ent[0]() is x and ent[1] == x._version:
-            return ent[2]
+        if (ent is not None and ent[0]() is x and ent[1] == x.data_ptr() and ent[2] == x._version
+                and ent[3] == _GENERATION[0]):
+            return ent[4]
     res = out if out is not None else TP(R, C, x.device, prec=prec)
     assert (res.R, res.C, res.prec) == (R, C, prec)
     _lib.check(_lib.lib().mm_gemm_tp_pack(PRECS[prec], _lib.ptr(x), R, C, x.stride(0), int(trans), res.ptr(),
@@ -71,7 +82,7 @@ def pack(x, out=None, trans=False, prec="x3"):
         d = _PACK_CACHE.get(id(x))
         if d is None or any(e[0]() is not x for e in d.values()):  # a new tensor at a reused id
             d = _PACK_CACHE[id(x)] = {}
-        d[key] = (weakref.ref(x), x._version, res)
+        d[key] = (weakref.ref(x), x.data_ptr(), x._version, _GENERATION[0], res)
     return res
 
 
@@ -155,6 +166,22 @@ def nt(a, b, bias=None, relu=False, mask=None, out=None, out_tp=None, want_f32=T
 def colsum_buf(M, N, device):
     """Per-16-row-tile column sums [ceil(M / 16), N] (bias-gradient partials)."""
     return torch.empty(((int(M) + 15) // 16, int(N)), dtype=torch.float32, device=device)
+
+
+def colsum(x, out=None, slabs=256):
+    """x [R, N] f32 -> column sums [N] (mm_colsum: two passes in a fixed order) -- the bias gradients,
+    from the GEMM epilogues' per-tile sums or straight from dY."""
+    x = x.contiguous()
+    R, N = x.shape
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=x.device)
+    if R == 0:
+        return out.zero_()
+    G = max(1, min(int(slabs), int(R) // 8))  # slabs of >= 8 rows
+    part = torch.empty((G, N), dtype=torch.float32, device=x.device) if G > 1 else None
+    _lib.check(_lib.lib().mm_colsum(_lib.ptr(x), int(R), int(N), _lib.ptr(part), G, _lib.ptr(out),
+                                    _lib.stream_ptr()), "mm_colsum")
+    return out
 
 
 def heads_bwd(dz, w, bits):

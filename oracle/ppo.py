@@ -61,13 +61,18 @@ def gae_fp32(rew, val, done, gamma=0.99, lam=0.95):
 # networks (networks.py)
 # ----------------------------------------------------------------------------
 class OProjection(nn.Module):
-    def __init__(self):
+    def __init__(self, parity=True):
         super().__init__()
         self.layers = nn.ModuleList([nn.Linear(d, EMB) for d in FEATURE_DIMS])
+        self.parity = parity
 
     def forward(self, x):
-        # networks.py:58-65 -- the slice start never advances (Q1)
-        outs = [lin(x[:, 0:d]) for lin, d in zip(self.layers, FEATURE_DIMS)]
+        # networks.py:58-65 -- the slice start never advances (Q1).  parity=False is NOT the
+        # reference: each feature reads its own slice x[:, s_i:s_i + d_i], s_i = sum of the earlier
+        # widths -- what the code evidently intended (the product's parity_mode=False); it has no
+        # reference counterpart to pin it, so tests use it only against the product.
+        starts = [0] * len(FEATURE_DIMS) if self.parity else list(np.cumsum([0] + FEATURE_DIMS[:-1]))
+        outs = [lin(x[:, s:s + d]) for lin, d, s in zip(self.layers, FEATURE_DIMS, starts)]
         return torch.cat(outs, dim=1).reshape(-1, len(FEATURE_DIMS), EMB)
 
 
@@ -88,9 +93,9 @@ class OAttention(nn.Module):
 
 
 class OActor(nn.Module):
-    def __init__(self, hidden=(264, 264, 264)):
+    def __init__(self, hidden=(264, 264, 264), parity=True):
         super().__init__()
-        self.projection = OProjection()
+        self.projection = OProjection(parity)
         self.attention = OAttention()
         sizes = [len(FEATURE_DIMS) * EMB] + list(hidden)
         self.layers = nn.ModuleList([nn.Linear(a, b) for a, b in zip(sizes[:-1], sizes[1:])])

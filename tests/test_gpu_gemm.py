@@ -29,7 +29,9 @@ def _rel_err(got, ref, scale):
 
 @pytest.mark.parametrize("prec", ["x3", "f16"])
 @pytest.mark.parametrize("M,N,K", [(419430, 264, 264), (70001, 264, 460), (40000, 6, 264), (209715, 64, 130),
-                                   (30000, 64, 64), (30000, 1, 64), (100, 264, 264), (1, 6, 264), (37, 5, 9)])
+                                   (30000, 64, 64), (30000, 1, 64), (100, 264, 264), (1, 6, 264), (37, 5, 9),
+                                   (1, 264, 460), (300, 264, 264), (6000, 264, 460), (8192, 264, 264),
+                                   (4096, 64, 130), (3000, 1, 64)])
 def test_wgrad_matches_fp64(prec, M, N, K):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     dy = torch.randn(M, N, device="cuda", generator=g)
@@ -70,11 +72,17 @@ def algo(request):
 @pytest.mark.parametrize("prec", ["x3", "f16"])
 @pytest.mark.parametrize("M,N,K", [(40000, 264, 460), (40000, 264, 264), (40000, 6, 264), (40000, 64, 130),
                                    (40000, 1, 64), (777, 64, 64), (40000, 460, 264), (16411, 264, 264),
-                                   (20000, 96, 52)])
+                                   (20000, 96, 52),
+                                   # the reference's own row counts: the single-sample API, main.py's 3,000-sample
+                                   # minibatches (6,000 actor rows), a 4,096-maze rollout step (8,192 actor rows)
+                                   (1, 264, 460), (2, 264, 264), (300, 264, 264), (300, 6, 264), (6000, 264, 460),
+                                   (6000, 460, 264), (8192, 264, 264), (8192, 6, 264), (4096, 64, 130), (3000, 1, 64)])
 def test_gemm_forward_and_input_gradient(prec, M, N, K, algo):
     """Forward (bias + ReLU + bit mask) and the input-gradient form (bits of the
     layer below, per-tile column sums) in both precisions, 16- and 8-byte rows,
-    both kernels; ragged M (16,411: a partial last row tile and 32-row unit), K
+    both kernels (below 16,384 rows both settings run the streaming kernel, with
+    4-tile column blocks where the row blocks alone would not fill the chip);
+    ragged M (16,411: a partial last row tile and 32-row unit), K
     with a 16-wide final step (264, 460, 130) or a partial 32-wide one (52); N = 460: no
     bit masks (N <= 272), the plain input-gradient form."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K)

@@ -381,7 +381,7 @@ def test_x3_relu_bits(M):
 
 @pytest.mark.parametrize("heads", [False, True])
 def test_x3_trunk_gradients_vs_fp64(heads):
-    """The actor MLP on the x3 GEMMs -- _X3Trunk (trunk) and _X3Actor (trunk +
+    """The actor MLP on the x3 GEMMs -- _EngineTrunk (trunk) and _EngineActor (trunk +
     heads: forward, ReLU bits, the fused heads backward, input / weight / bias
     gradients with the bias sums from the GEMM epilogues) -- against an fp64
     evaluation linearised at the same ReLU pattern (a ReLU whose input is within
@@ -390,7 +390,7 @@ def test_x3_trunk_gradients_vs_fp64(heads):
     under test).  Tolerance: 1e-6 of max|ref| for outputs, 2e-5 for gradients
     (sums over 40,000 rows)."""
     from marlmaze import x3
-    from marlmaze.networks import Actor, _X3Actor, _X3Trunk
+    from marlmaze.networks import Actor, _EngineActor, _EngineTrunk
 
     torch.manual_seed(1)
     actor = Actor([264, 264, 264]).cuda()
@@ -402,11 +402,11 @@ def test_x3_trunk_gradients_vs_fp64(heads):
         wh.mul_(100.0)  # heads at the scale of the hidden layers (init is x0.01)
     if heads:
         dout = torch.randn(M, 6, device="cuda")
-        out = _X3Actor.apply(h0, wh, bh, *params)
+        out = _EngineActor.apply("x3", h0, wh, bh, *params)
         inputs = [h0, wh, bh] + params
     else:
         dout = torch.randn(M, 264, device="cuda")
-        out = _X3Trunk.apply(h0, *params)
+        out = _EngineTrunk.apply("x3", h0, *params)
         inputs = [h0] + params
     got = [out.detach()] + list(torch.autograd.grad(out, inputs, dout))
     pattern = []  # the x3 forward's ReLU pattern (the same GEMMs the functions run)
@@ -467,19 +467,3 @@ def test_fused_policy_loss_matches_torch(M):
     got, = torch.autograd.grad(loss, z2)
     assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item()) + 1e-7, (loss.item(), ref.item())
     assert (got - gref).abs().max().item() <= 1e-6 * gref.abs().max().item() + 1e-9
-
-
-@pytest.mark.parametrize("M,N,K", [(419430, 264, 460), (16 * 4096, 6, 264), (70001, 7, 13)])
-def test_split_k_wgrad_matches_fp64(M, N, K):
-    """networks._split_k_wgrad (batched split-K GEMM + mm_sum_leading, incl. the
-    remainder rows and the unaligned scalar path) against an fp64 dY^T X."""
-    from marlmaze.networks import _split_k_wgrad
-
-    g = torch.Generator(device="cuda").manual_seed(M)
-    dy = torch.randn(M, N, device="cuda", generator=g)
-    x = torch.randn(M, K, device="cuda", generator=g)
-    dw = _split_k_wgrad(dy, x)
-    ref = dy.double().t().mm(x.double())
-    scale = dy.double().abs().t().mm(x.double().abs())
-    err = ((dw.double() - ref).abs() / scale).max().item()
-    assert dw.shape == (N, K) and err < 1e-5, err

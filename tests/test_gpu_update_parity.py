@@ -59,8 +59,8 @@ def _agent(**kw):
     return PPO(2, **kw)
 
 
-def _oracle_nets(fx, dtype=torch.float32):
-    a, c = oppo.OActor(), oppo.OCritic()
+def _oracle_nets(fx, dtype=torch.float32, parity=True):
+    a, c = oppo.OActor(parity=parity), oppo.OCritic()
     a.load_state_dict({k[6:]: torch.as_tensor(fx[k]) for k in fx.files if k.startswith("actor/")})
     c.load_state_dict({k[7:]: torch.as_tensor(fx[k]) for k in fx.files if k.startswith("critic/")})
     return a.to(dtype), c.to(dtype)
@@ -114,15 +114,20 @@ def _check_delta(before, after, ref_before, ref_after, ref_grad, coef, tag, ulps
             assert excess.max().item() <= 0, (tag, k, excess.max().item(), int(sel.sum()), sel.numel())
 
 
-def _minibatch(fx, S):
+def _minibatch(fx, S, noise=0.0):
     """S samples: the fixture's rows tiled, with fresh advantages, returns and
-    old log-probs so that the rows differ."""
-    if S == fx["obs"].shape[0]:
+    old log-probs so that the rows differ; noise > 0 also perturbs every
+    observation (so that every row -- not only the 256 fixture rows -- is a
+    distinct input)."""
+    if S == fx["obs"].shape[0] and not noise:
         return tuple(torch.as_tensor(fx[k]) for k in ("obs", "actions", "old_logp", "advs", "rtgs", "masks"))
     g = torch.Generator().manual_seed(S)
     idx = torch.arange(S) % fx["obs"].shape[0]
     old = torch.as_tensor(fx["old_logp"])[idx] + 0.3 * torch.randn(S, generator=g)
-    return (torch.as_tensor(fx["obs"])[idx], torch.as_tensor(fx["actions"])[idx], old,
+    obs = torch.as_tensor(fx["obs"])[idx]
+    if noise:
+        obs = obs + noise * torch.randn(obs.shape, generator=g)
+    return (obs, torch.as_tensor(fx["actions"])[idx], old,
             torch.randn(S, generator=g), torch.randn(S, generator=g), torch.as_tensor(fx["masks"])[idx])
 
 
@@ -278,3 +283,87 @@ def test_config1_rollout_and_update_4096_mazes(golden):
     # rollout actor inputs are the 4 facing one-hots (quirk Q1), so the minibatch's gradient sums
     # collapse onto 4 activation vectors and cancel; see the module doc for the 2e-5 here
     _step_and_compare(ag, actor, critic, batch, "configs[1]", grad_rel=2e-5)
+
+
+def test_main_py_hyperparameters_minibatch(golden):
+    """The drop-in of INTEGRATION.md section 1, main.py:17 -- PPO(agent_amount=2,
+    batch_size=15000, lr=0.00014): its minibatch is 15000 // 5 = 3,000 samples
+    (PPO.py:27), i.e. 6,000 actor rows and 3,000 critic rows, all on the
+    hand-written engine (no library GEMM at any row count).  Gradients, losses,
+    norms and the Adam step vs the oracle at the 1e-5 bar."""
+    fx = golden("nets")
+    ag = _agent(n_envs=64, batch_size=15000)
+    assert ag.mbatch_size == 3000
+    actor, critic = _oracle_nets(fx)
+    _to_gpu(ag, actor, critic)
+    _step_and_compare(ag, actor, critic, _minibatch(fx, 3000), "main.py minibatch")
+
+
+@pytest.mark.parametrize("S", [3000, 32768])
+def test_minibatch_parity_mode_false(golden, S):
+    """parity_mode=False (each feature embedding reads its own slice of the
+    observation: the slicing networks.py:59-63 evidently intends; the oracle's
+    OActor(parity=False) restates it -- no reference counterpart, so the oracle
+    is the only anchor): every observation perturbed so that all S rows are
+    distinct inputs to the whole actor (not 4 one-hot classes, Q1).  The full
+    update -- gradients of every parameter, losses, norms, Adam step -- vs the
+    oracle at the 1e-5 bar."""
+    fx = golden("nets")
+    ag = _agent(n_envs=64, parity_mode=False)
+    actor, critic = _oracle_nets(fx, parity=False)
+    _to_gpu(ag, actor, critic)
+    _step_and_compare(ag, actor, critic, _minibatch(fx, S, noise=0.5), f"parity_mode=False S={S}")
+
+
+def test_rollout_forward_4096_mazes_matches_oracle(golden):
+    """BASELINE configs[1]'s rollout forward: the critic on the 4,096 mazes'
+    [4096, 130] observations and the actor (trunk + heads) on their 8,192 agent
+    rows, at the shipped checkpoint's weights (ckpt_logits.npz) and at 1e-5 of
+    the fp32 oracle; the fused head + sampler kernel's logits too."""
+    from marlmaze import ops
+
+    c = golden("ckpt_logits")
+    n = 4096
+    ag = _agent(n_envs=n, horizon=4, env_config=dict(default_size=(10, 10), max_timestep=1200, seed_base=0))
+    ag.actor.load_state_dict({k[6:]: torch.as_tensor(c[k]) for k in c.files if k.startswith("actor/")})
+    ag.critic.load_state_dict({k[7:]: torch.as_tensor(c[k]) for k in c.files if k.startswith("critic/")})
+    actor, critic = oppo.OActor(), oppo.OCritic()
+    actor.load_state_dict({k: v.cpu() for k, v in ag.actor.state_dict().items()})
+    critic.load_state_dict({k: v.cpu() for k, v in ag.critic.state_dict().items()})
+    ag._ensure_env()
+    obs = ag._bufs["obs"][0]
+    masks = ag._bufs["masks"][0]
+    with torch.no_grad():
+        v = ag.critic(obs).cpu()
+        mv, mk = ag.actor(obs.reshape(2 * n, 65))
+        h = ag.actor.trunk(obs.reshape(2 * n, 65))
+        w, b = ag.actor.heads()
+        lg = torch.empty(2 * n, 6, device="cuda")
+        ops.head_sample(h, w, b, masks.reshape(2 * n, 6), 1, 0, logits=lg)
+        rv = critic(obs.cpu())
+        rmv, rmk = actor(obs.cpu().reshape(2 * n, 65))
+    for got, ref, what in ((v, rv, "values"), (mv.cpu(), rmv, "move"), (mk.cpu(), rmk, "mark"),
+                           (lg[:, :5].cpu(), rmv, "head_sample move"), (lg[:, 5:].cpu(), rmk, "head_sample mark")):
+        err = (got.double() - ref.double()).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item() + 1e-6, (what, err)
+
+
+def test_update_calls_no_library_gemm(golden, monkeypatch):
+    """Every GEMM of the update -- at main.py's 3,000-sample minibatch -- and of
+    a 4,096-maze rollout runs on the hand-written kernels: the torch GEMM entry
+    points are poisoned for the duration."""
+    def boom(*a, **k):
+        raise AssertionError("a library GEMM was called on the product path")
+
+    import torch.nn.functional as F
+    fx = golden("nets")
+    ag = _agent(n_envs=4096, horizon=2, batch_size=15000,
+                env_config=dict(default_size=(10, 10), max_timestep=1200, seed_base=0))
+    batch = [t.cuda() for t in _minibatch(fx, 3000)]
+    for mod, name in ((torch, "mm"), (torch, "addmm"), (torch, "bmm"), (torch, "matmul"), (torch, "_addmm_activation"),
+                      (F, "linear"), (torch.Tensor, "mm"), (torch.Tensor, "matmul"), (torch.Tensor, "__matmul__"),
+                      (torch.Tensor, "addmm")):
+        monkeypatch.setattr(mod, name, boom)
+    ag.rollout()
+    ag.minibatch_step(*batch)
+    torch.cuda.synchronize()

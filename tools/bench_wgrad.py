@@ -1,6 +1,6 @@
 """Weight-gradient GEMM timings (HIP events) at the update's shapes: the
-hand-written mm_gemm_wgrad (x3, f16) against the library split-K path it
-replaces (networks._split_k_wgrad: hipBLASLt batched GEMM + mm_sum_leading)."""
+hand-written mm_gemm_wgrad (x3, f16) against the fp32 library GEMM
+(torch dY^T X on hipBLASLt) that it replaced."""
 import os
 import sys
 
@@ -8,10 +8,6 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "marl-maze_amd"))
 from marlmaze import x3  # noqa: E402
-from marlmaze.gemm_tuning import enable_tuned_gemms  # noqa: E402
-from marlmaze.networks import _split_k_wgrad  # noqa: E402
-
-enable_tuned_gemms()
 
 
 def t(f, n=10):
@@ -32,7 +28,7 @@ for M, N, K in ((419430, 264, 264), (419430, 264, 460), (419430, 6, 264), (20971
     x = torch.randn(M, K, device="cuda")
     fl = 2.0 * M * N * K
     r = [f"M={M} {N}x{K}:"]
-    for name, f in (("lib", lambda: _split_k_wgrad(dy, x)), ("x3", lambda: x3.wgrad(dy, x)),
+    for name, f in (("lib", lambda: dy.t().mm(x)), ("x3", lambda: x3.wgrad(dy, x)),
                     ("f16", lambda: x3.wgrad(dy, x, prec="f16"))):
         us = t(f)
         r.append(f"{name} {us:8.1f} us ({fl / us / 1e6:6.1f} TF/s, {4.0 * M * (N + K) / us / 1e3:6.0f} GB/s)")
