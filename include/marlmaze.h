@@ -355,6 +355,13 @@ int mm_clip_adam(const mm_adam_seg_t* segs, int nseg, float beta1, float beta2, 
 int mm_head_sample(const float* h, int ldh, int K, const float* w, const float* b, const uint8_t* masks, int M,
                    uint64_t seed, uint64_t offset, int8_t* actions, float* logp, float* joint_logp, float* logits,
                    void* stream);
+/* mm_head_sample whose Philox counter offset is offset + *offset_dev (offset_dev a
+ * device uint64, may be NULL): a captured HIP graph of the rollout bakes the
+ * host argument in, so each replay reads its base offset from the device and
+ * advances it there -- the same draws as the uncaptured rollout. */
+int mm_head_sample_ex(const float* h, int ldh, int K, const float* w, const float* b, const uint8_t* masks, int M,
+                      uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int8_t* actions, float* logp,
+                      float* joint_logp, float* logits, void* stream);
 
 /* Actor front-end, fused (networks.py:31-34,51-82): the 23 feature embeddings
  * (Projection; parity != 0 keeps quirk Q1, every embedding reads x[:, 0:d_i]),

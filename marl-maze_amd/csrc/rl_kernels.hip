@@ -310,6 +310,7 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* 
                                                                    const float* __restrict__ b,
                                                                    const uint8_t* __restrict__ masks, int M,
                                                                    uint64_t seed, uint64_t offset,
+                                                                   const uint64_t* __restrict__ offset_dev,
                                                                    int8_t* __restrict__ act, float* __restrict__ logp,
                                                                    float* __restrict__ joint,
                                                                    float* __restrict__ logits) {
@@ -360,7 +361,8 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* 
         for (int o = 0; o < 5; o++) l[o] = acc[o] + b[o];
         const float kl = acc[5] + b[5];
         int move, mark;
-        lp = sample_row(l, kl, masks + (size_t)row * MM_MASK_DIM, row, seed, offset, move, mark);
+        const uint64_t off = offset + (offset_dev ? *offset_dev : 0ull);  // a device base: graph replays advance it
+        lp = sample_row(l, kl, masks + (size_t)row * MM_MASK_DIM, row, seed, off, move, mark);
         act[2 * row] = (int8_t)move;
         act[2 * row + 1] = (int8_t)mark;
         if (logp) logp[row] = lp;
@@ -508,17 +510,25 @@ extern "C" int mm_sample(const float* move_logits, const float* mark_logits, con
     return (int)hipGetLastError();
 }
 
-extern "C" int mm_head_sample(const float* h, int ldh, int K, const float* w, const float* b, const uint8_t* masks,
-                              int M, uint64_t seed, uint64_t offset, int8_t* actions, float* logp, float* joint_logp,
-                              float* logits, void* stream) {
+extern "C" int mm_head_sample_ex(const float* h, int ldh, int K, const float* w, const float* b,
+                                 const uint8_t* masks, int M, uint64_t seed, uint64_t offset,
+                                 const uint64_t* offset_dev, int8_t* actions, float* logp, float* joint_logp,
+                                 float* logits, void* stream) {
     if (!h || !w || !b || !masks || !actions || M < 0 || K <= 0 || (K & 3) || K > kHsMaxK || ldh < K || (ldh & 3) ||
         ((uintptr_t)h & 15))
         return MM_E_ARG;
     if (M == 0) return 0;
     hipLaunchKernelGGL(k_head_sample, dim3((M + kHsRows - 1) / kHsRows), dim3(kHsLanes * kHsRows), 0,
-                       (hipStream_t)stream, h, ldh, K, w, b, masks, M, seed, offset, actions, logp, joint_logp,
-                       logits);
+                       (hipStream_t)stream, h, ldh, K, w, b, masks, M, seed, offset, offset_dev, actions, logp,
+                       joint_logp, logits);
     return (int)hipGetLastError();
+}
+
+extern "C" int mm_head_sample(const float* h, int ldh, int K, const float* w, const float* b, const uint8_t* masks,
+                              int M, uint64_t seed, uint64_t offset, int8_t* actions, float* logp, float* joint_logp,
+                              float* logits, void* stream) {
+    return mm_head_sample_ex(h, ldh, K, w, b, masks, M, seed, offset, nullptr, actions, logp, joint_logp, logits,
+                             stream);
 }
 
 extern "C" int mm_ppo_loss_partials(int M) { return (M + kLossThreads - 1) / kLossThreads; }

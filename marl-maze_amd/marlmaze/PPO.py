@@ -97,7 +97,7 @@ class PPO:
                  updates_per_batch=5, clip=0.2, max_grad=0.5, *, n_envs=4096, horizon=None, env_config=None,
                  seed=3234, sample_seed=None, device=None, model_path=MODEL_PATH, load=True, parity_mode=True,
                  bootstrap=True, dp=None, verbose=True, save=True, episode_batches=False,
-                 episode_chunk=64, dtype="f32"):
+                 episode_chunk=64, dtype="f32", graph_rollout=False):
         self.maze = None  # wired by Maze.__init__ (maze.py:39-42), as in the reference
         self.dp = dp if dp is not None else DP.single()
         if device is None:
@@ -166,6 +166,15 @@ class PPO:
         self._bufs = None
         self.history = []
         self.step_events = None  # list -> rollout records (start, end) events around each env step
+        # capture the fixed-horizon rollout (every step's critic, actor trunk, head + sampler, env step and
+        # the GAE) in one HIP graph and replay it: at a few thousand mazes the ~15 launches per step are
+        # host-bound, a replay is one launch
+        self.graph_rollout = bool(graph_rollout)
+        self._graph = None
+        self._graph_key = None
+        self._graph_warm = False
+        self._ctr = None  # device base of the sampler's Philox offset in graph replays
+        self._ctr_val = None
         if load:
             self.load_parameters()
 
@@ -215,19 +224,53 @@ class PPO:
         """Advance every maze ``horizon`` steps; fills the [T, N] buffers."""
         self._ensure_env()
         b, n, T = self._bufs, self.n_envs, self.horizon
+        if self.graph_rollout and self.step_events is None and self.device.type == "cuda":
+            return self._rollout_graph(b, n, T)
         with x3.cached_packs():  # the weights are fixed during the rollout: pack them once, not per step
             return self._rollout_steps(b, n, T)
 
-    def _rollout_steps(self, b, n, T):
+    def _rollout_graph(self, b, n, T):
+        """The rollout as a replay of a captured HIP graph (same kernels, same
+        draws: the sampler reads its Philox base offset from the device)."""
+        key = (id(self.venv), self.flat.data.data_ptr() if self.flat is not None else None, T, id(b["obs"]))
+        if self._graph is None or self._graph_key != key:
+            if not self._graph_warm:  # the first rollout runs uncaptured (one-time host work: kernel attributes)
+                self._graph_warm = True
+                with x3.cached_packs():
+                    return self._rollout_steps(b, n, T)
+            self._graph = torch.cuda.CUDAGraph()
+            self._ctr = torch.tensor([self._sample_offset], dtype=torch.int64, device=self.device)
+            self._ctr_val = self._sample_offset
+            torch.cuda.synchronize(self.device)
+            self.venv.capturing = True
+            try:
+                with torch.cuda.graph(self._graph):
+                    with x3.cached_packs():
+                        self._rollout_steps(b, n, T, offset_dev=self._ctr)
+                    self._ctr += T
+            finally:
+                self.venv.capturing = False
+            self._graph_key = key
+        if self._ctr_val != self._sample_offset:  # an uncaptured rollout ran in between
+            self._ctr.fill_(self._sample_offset)
+        self._graph.replay()
+        self._sample_offset += T
+        self._ctr_val = self._sample_offset
+        self.venv._kick_pregen()  # refill the next mazes the replay's resets consumed
+        return b
+
+    def _rollout_steps(self, b, n, T, offset_dev=None):
         head_w, head_b = self.actor.heads()
         for t in range(T):
             obs_t = b["obs"][t]
             b["val"][t] = self.critic(obs_t).view(n)
             # actor trunk, then heads + sampling fused (PPO.py:170-186; ops.head_sample)
             h = self.actor.trunk(obs_t.view(2 * n, 65))
-            ops.head_sample(h, head_w, head_b, b["masks"][t].view(2 * n, 6), self.sample_seed, self._sample_offset,
-                            actions=b["act"][t].view(2 * n, 2), logp=b["rowlogp"][t], joint_logp=b["logp"][t])
-            self._sample_offset += 1
+            ops.head_sample(h, head_w, head_b, b["masks"][t].view(2 * n, 6), self.sample_seed,
+                            t if offset_dev is not None else self._sample_offset, actions=b["act"][t].view(2 * n, 2),
+                            logp=b["rowlogp"][t], joint_logp=b["logp"][t], offset_dev=offset_dev)
+            if offset_dev is None:
+                self._sample_offset += 1
             ev = self.step_events
             if ev is None:
                 self.venv.step(b["act"][t], auto_reset=True, obs=b["obs"][t + 1], masks=b["masks"][t + 1],

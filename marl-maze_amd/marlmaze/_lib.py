@@ -34,7 +34,7 @@ AF_HAS_MARK = 64
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
-           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample",
+           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample", "mm_head_sample_ex",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd", "mm_actor_front_fwd_ex",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd", "mm_actor_front_bwd_ex",
            "mm_actor_front_bwd_to",
@@ -115,6 +115,8 @@ def lib():
         L.mm_sample.restype = i32
         L.mm_head_sample.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P]
         L.mm_head_sample.restype = i32
+        L.mm_head_sample_ex.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P, P]
+        L.mm_head_sample_ex.restype = i32
         L.mm_x3_tp_len.argtypes = [i32, i32]
         L.mm_x3_tp_len.restype = ctypes.c_long
         L.mm_x3_tp_pack.argtypes = [P, i32, i32, i32, i32, P, P]

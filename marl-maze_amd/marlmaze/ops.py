@@ -64,12 +64,15 @@ def sample(move_logits, mark_logits, masks, seed, offset, actions=None, logp=Non
     return actions, logp, joint_logp
 
 
-def head_sample(h, head_w, head_b, masks, seed, offset, actions=None, logp=None, joint_logp=None, logits=None):
+def head_sample(h, head_w, head_b, masks, seed, offset, actions=None, logp=None, joint_logp=None, logits=None,
+                offset_dev=None):
     """Actor heads + PPO.get_action in one kernel (csrc/rl_kernels.hip k_head_sample).
 
     h [M, K] f32 (last hidden layer), head_w [6, K] = [move_head.weight;
     mark_head.weight], head_b [6], masks [M, 6] u8.  Same draws as ``sample``
-    on the same (seed, offset, row).  Returns actions, logp, joint_logp.
+    on the same (seed, offset, row); offset_dev (a device int64 [1], optional)
+    adds a device-side base to ``offset`` (HIP-graph replays).  Returns
+    actions, logp, joint_logp.
     """
     M, K = h.shape
     dev = h.device
@@ -83,8 +86,9 @@ def head_sample(h, head_w, head_b, masks, seed, offset, actions=None, logp=None,
         logp = torch.empty(M, dtype=torch.float32, device=dev)
     if joint_logp is None:
         joint_logp = torch.empty((M + 1) // 2, dtype=torch.float32, device=dev)
-    _lib.check(_lib.lib().mm_head_sample(_lib.ptr(hc), int(hc.stride(0)), int(K), _lib.ptr(w), _lib.ptr(b),
-                                         _lib.ptr(mk), int(M), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
-                                         _lib.ptr(actions), _lib.ptr(logp), _lib.ptr(joint_logp), _lib.ptr(logits),
-                                         _lib.stream_ptr()), "mm_head_sample")
+    _lib.check(_lib.lib().mm_head_sample_ex(_lib.ptr(hc), int(hc.stride(0)), int(K), _lib.ptr(w), _lib.ptr(b),
+                                            _lib.ptr(mk), int(M), int(seed) & (2**64 - 1), int(offset) & (2**64 - 1),
+                                            _lib.ptr(offset_dev), _lib.ptr(actions), _lib.ptr(logp),
+                                            _lib.ptr(joint_logp), _lib.ptr(logits), _lib.stream_ptr()),
+               "mm_head_sample_ex")
     return actions, logp, joint_logp

@@ -79,6 +79,9 @@ class VecMaze:
         # pre-generation (mm_env_pregen): each maze's next maze is generated ahead on a side stream,
         # so a reset is a copy (the serial backtracker leaves the step's critical path)
         self.pregen = bool(pregen) and os.environ.get("MARLMAZE_PREGEN", "1") != "0"
+        # True while a HIP graph captures steps: the side-stream pre-generation is then kicked by the
+        # caller after each replay instead (a captured fork must rejoin its origin stream)
+        self.capturing = False
         if self.pregen:
             self.next_layout = torch.ones((self.n, stride), dtype=torch.uint8, device=d)
             self.next_mazes = torch.zeros((self.n, 32), dtype=torch.uint8, device=d)
@@ -108,7 +111,7 @@ class VecMaze:
         on the current stream (the resets that left mazes pending).  The current
         stream never waits for it: a reset whose next maze is not ready yet
         generates it itself, or waits for the one in flight (gen_state)."""
-        if not self.pregen:
+        if not self.pregen or self.capturing:
             return
         cur = torch.cuda.current_stream(self.device)
         self._gen_stream.wait_stream(cur)

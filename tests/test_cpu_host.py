@@ -110,57 +110,92 @@ import numpy as np, torch
 import torch.distributed as dist
 from marlmaze.dist import DP
 from marlmaze.PPO import PPO
-rank = int(sys.argv[1]); world = 2
-os.environ.update(RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+rank, world = int(sys.argv[1]), int(sys.argv[5])
+os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
 dp = DP.from_env(backend="gloo")
 torch.set_num_threads(1)
 data = np.load(sys.argv[3])
-Bl = data["obs"].shape[0] // 2
+Bl = data["obs"].shape[0] // world
 sl = slice(rank * Bl, (rank + 1) * Bl)
-ag = PPO(2, batch_size=2 * Bl - (2 * Bl) % 10, lr=1e-6, device="cpu", dp=dp, load=False, verbose=False, save=False)
+ag = PPO(2, batch_size=world * Bl - (world * Bl) % (5 * world), lr=1e-6, device="cpu", dp=dp, load=False,
+         verbose=False, save=False)
 hist = ag.update(*(torch.as_tensor(data[k][sl]) for k in ("obs", "act", "logp", "masks", "adv", "val")),
                  index_list=data["idx%d" % rank])
-if rank == 0:
-    np.savez(sys.argv[4], hist=hist.numpy(), **{{k: v.numpy() for k, v in ag.actor.state_dict().items()}})
+out = dict(hist=hist.numpy(), **{{k: v.numpy() for k, v in ag.actor.state_dict().items()}},
+           **{{"critic." + k: v.numpy() for k, v in ag.critic.state_dict().items()}})
+np.savez(sys.argv[4] + "_%d.npz" % rank, **out)
 dist.destroy_process_group()
 """
 
 
-def test_data_parallel_update_equals_single_process(tmp_path, golden):
-    """2 gloo ranks, each with half the batch and its own shuffle, give the
-    same losses/parameters as one process whose minibatches are the unions."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_update_equals_single_process(tmp_path, golden, world):
+    """``world`` gloo ranks, each with 1/world of the batch and its own shuffle,
+    give the same losses and parameters as one process whose minibatches are
+    the unions (results independent of the world size), and
+    every rank ends with the same parameters bit for bit."""
     from marlmaze.PPO import PPO
 
     t = golden("train_small")
-    B = 640  # 2 ranks x 320
-    rng = np.random.default_rng(0)
+    B = 640
+    rng = np.random.default_rng(world)
     data = dict(obs=t["obs"][:B], act=t["actions"][:B], logp=t["logp"][:B], masks=t["masks"][:B],
                 adv=t["advs"][:B], val=t["vals"][:B])
-    Bl = B // 2
-    idx = [rng.permutation(Bl) for _ in range(2)]
+    Bl = B // world
+    idx = [rng.permutation(Bl) for _ in range(world)]
     fx = str(tmp_path / "dp_in.npz")
-    np.savez(fx, idx0=idx[0], idx1=idx[1], **data)
+    np.savez(fx, **{f"idx{r}": idx[r] for r in range(world)}, **data)
     port = str(_free_port())
-    out = str(tmp_path / "dp_out.npz")
+    out = str(tmp_path / "dp_out")
     script = str(tmp_path / "worker.py")
     open(script, "w").write(_DP_WORKER.format(pkg=os.path.join(REPO, "marl-maze_amd"), repo=REPO))
-    procs = [subprocess.Popen([sys.executable, script, str(r), port, fx, out]) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, script, str(r), port, fx, out, str(world)]) for r in range(world)]
     for p in procs:
         assert p.wait(timeout=300) == 0
-    got = np.load(out)
-    # single process: minibatch k = rank0 slice k  U  rank1 slice k
+    got = [np.load(out + f"_{r}.npz") for r in range(world)]
+    for r in range(1, world):  # parameters identical on every rank
+        for k in got[0].files:
+            if k != "hist":
+                assert np.array_equal(got[r][k], got[0][k]), (r, k)
+    # single process: minibatch k = the union over ranks of slice k
     local_bs = Bl - Bl % 5
     mb_l = local_bs // 5
     glob = []
     for k in range(5):
-        glob += list(idx[0][k * mb_l:(k + 1) * mb_l]) + list(Bl + idx[1][k * mb_l:(k + 1) * mb_l])
+        for r in range(world):
+            glob += list(r * Bl + idx[r][k * mb_l:(k + 1) * mb_l])
     torch.set_num_threads(1)
-    ag = PPO(2, batch_size=2 * local_bs, lr=1e-6, device="cpu", load=False, verbose=False, save=False)
+    ag = PPO(2, batch_size=world * local_bs, lr=1e-6, device="cpu", load=False, verbose=False, save=False)
     hist = ag.update(*(torch.as_tensor(data[k]) for k in ("obs", "act", "logp", "masks", "adv", "val")),
                      index_list=np.asarray(glob))
-    np.testing.assert_allclose(got["hist"][:, :2], hist.numpy()[:, :2], rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(got[0]["hist"][:, :2], hist.numpy()[:, :2], rtol=2e-5, atol=1e-6)
     for k, v in ag.actor.state_dict().items():
-        np.testing.assert_allclose(got[k], v.numpy(), rtol=0, atol=3e-6)
+        np.testing.assert_allclose(got[0][k], v.numpy(), rtol=0, atol=3e-6)
+    for k, v in ag.critic.state_dict().items():
+        np.testing.assert_allclose(got[0]["critic." + k], v.numpy(), rtol=0, atol=3e-6)
+
+
+def test_integration_struct_matches_header():
+    """INTEGRATION.md section 2's ctypes mirror of mm_env_t has the header's 19
+    fields at the header's offsets (the binding a maintainer copies must not be
+    shorter than the struct the library reads), and the library reports the
+    same size (mm_env_desc_size) and ABI major version."""
+    import ctypes
+
+    _ensure_lib()
+    md = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(import ctypes, torch.*?)```", md, re.S).group(1)
+    cls = re.search(r"(class mm_env_t\(ctypes\.Structure\):.*?\])\n\n", block, re.S).group(1)
+    ns = {"ctypes": ctypes}
+    exec(cls, ns)
+    T = ns["mm_env_t"]
+    names = [f for f, _ in T._fields_]
+    assert len(names) == 19 and names == [f for f, _ in _lib.EnvDesc._fields_]
+    assert [getattr(T, f).offset for f in names] == [getattr(_lib.EnvDesc, f).offset for f in names]
+    L = _lib.lib()
+    assert ctypes.sizeof(T) == L.mm_env_desc_size() == ctypes.sizeof(_lib.EnvDesc)
+    assert L.mm_version() // 100 == _lib.VERSION // 100 == 3
+    assert "mm_env_desc_size() == ctypes.sizeof(mm_env_t)" in block
 
 
 @pytest.mark.parametrize("world", [2])

@@ -96,3 +96,35 @@ def test_main_py_wiring_trains():
     assert env.max_timestep == 60 and env.rand_sizes and env.rand_start
     assert set(np.unique(info["w"]).tolist()) <= {23, 25} and not info["status"].any()
     assert len(brain.history) == 1 and np.isfinite(brain.history[0]["actor_loss"])
+
+
+def test_integration_snippet_runs():
+    """INTEGRATION.md section 2's ctypes block, executed as written from the
+    repository root (its asserts: every call returns 0, pre-generation off), and
+    its reset observations equal the package's own VecMaze for the same seeds."""
+    import os
+    import re
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    md = open(os.path.join(repo, "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(import ctypes, torch.*?)```", md, re.S).group(1)
+    cwd = os.getcwd()
+    os.chdir(repo)
+    try:
+        ns = {}
+        exec(compile(block, "INTEGRATION.md", "exec"), ns)
+    finally:
+        os.chdir(cwd)
+    import torch
+
+    from marlmaze.vecmaze import VecMaze
+
+    N = ns["N"]
+    env = VecMaze(N, default_size=(10, 10), max_timestep=1200, seeds=list(range(N)), pregen=False)
+    env.reset()
+    # the snippet stepped once with "stay": the same step through the package
+    act = torch.zeros(N, 2, 2, dtype=torch.int8, device="cuda")
+    act[..., 0] = 4
+    o1, m1, r1, _ = env.step(act, auto_reset=True)
+    assert torch.equal(o1, ns["obs"]) and torch.equal(m1.to(torch.uint8), ns["masks"])
+    assert torch.equal(r1, ns["reward"])

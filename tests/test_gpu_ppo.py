@@ -467,3 +467,31 @@ def test_fused_policy_loss_matches_torch(M):
     got, = torch.autograd.grad(loss, z2)
     assert abs(loss.item() - ref.item()) <= 1e-6 * abs(ref.item()) + 1e-7, (loss.item(), ref.item())
     assert (got - gref).abs().max().item() <= 1e-6 * gref.abs().max().item() + 1e-9
+
+
+@pytest.mark.parametrize("n", [512, 4096])
+def test_graph_rollout_equals_eager(n):
+    """PPO(graph_rollout=True) -- the fixed-horizon rollout captured once as a HIP
+    graph and replayed (the sampler's Philox base offset read from the device)
+    -- gives bit-identical batches to the uncaptured rollout over several
+    iterations (episodes and auto-resets crossing the batches), including after
+    an update changed the weights the graph reads in place."""
+    cfg = dict(default_size=(6, 6), max_timestep=20, seed_base=7)
+    T = 8
+    ags = [_agent(n_envs=n, horizon=T, batch_size=n * T, sample_seed=5, env_config=cfg, graph_rollout=g)
+           for g in (False, True)]
+    for it in range(4):
+        outs = []
+        for ag in ags:
+            b = ag.rollout()
+            outs.append({k: b[k].clone() for k in ("obs", "masks", "act", "logp", "val", "rew", "done", "adv", "rtg")})
+            if it == 1:  # one update step: the captured graph must see the new weights
+                B = T * n
+                idx = torch.arange(B, device="cuda")[: B // 5]
+                ag.minibatch_step(b["obs"][:T].reshape(B, 2, 65)[idx], b["act"].reshape(B, 2, 2)[idx],
+                                  b["logp"].reshape(B)[idx], b["adv"].reshape(B)[idx], b["rtg"].reshape(B)[idx],
+                                  b["masks"][:T].reshape(B, 2, 6)[idx])
+            ag._carry_over()
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], outs[1][k]), (it, k)
+    assert ags[1]._graph is not None and ags[0]._sample_offset == ags[1]._sample_offset
