@@ -107,11 +107,16 @@ class OActor(nn.Module):
             self.move_head.weight *= 0.01
             self.mark_head.weight *= 0.01
 
-    def forward(self, x):  # networks.py:31-41
+    def forward(self, x, relu_masks=None):  # networks.py:31-41
+        """relu_masks (tests only, no reference counterpart): per hidden layer a bool
+        [rows, width] pattern replacing ReLU by the linear map on that pattern --
+        the network linearised at another evaluation's ReLU pattern (a ReLU whose
+        input is within rounding of 0 may fall on either side under a different
+        summation order)."""
         x = torch.as_tensor(x, dtype=self.move_head.weight.dtype).reshape(-1, OBS)
         x = self.attention(self.projection(x))
-        for lin in self.layers:
-            x = torch.relu(lin(x))
+        for l, lin in enumerate(self.layers):
+            x = torch.relu(lin(x)) if relu_masks is None else lin(x) * relu_masks[l].to(x.dtype)
         return [self.move_head(x), self.mark_head(x)]
 
 
@@ -124,10 +129,10 @@ class OCritic(nn.Module):
         for lin in self.layers:  # networks.py:104-106
             nn.init.orthogonal_(lin.weight)
 
-    def forward(self, x):  # networks.py:96-102
+    def forward(self, x, relu_masks=None):  # networks.py:96-102 (relu_masks: as OActor.forward)
         x = torch.as_tensor(x, dtype=self.layers[0].weight.dtype).reshape(-1, self.agent_amount * OBS)
-        for lin in self.layers[:-1]:
-            x = torch.relu(lin(x))
+        for l, lin in enumerate(self.layers[:-1]):
+            x = torch.relu(lin(x)) if relu_masks is None else lin(x) * relu_masks[l].to(x.dtype)
         return self.layers[-1](x)
 
 
@@ -140,10 +145,11 @@ def make_nets(seed=3234):
 # ----------------------------------------------------------------------------
 # PPO pieces
 # ----------------------------------------------------------------------------
-def log_probs(actor, i, obs, act, masks):
-    """PPO.get_log_probs (PPO.py:154-168)."""
+def log_probs(actor, i, obs, act, masks, relu_masks=None):
+    """PPO.get_log_probs (PPO.py:154-168).  relu_masks: the actor's patterns over
+    the interleaved [2M] agent rows (row 2m + i), see OActor.forward."""
     moves, marks = act[:, i, 0], act[:, i, 1]
-    ml, kl = actor(obs[:, i, :])
+    ml, kl = actor(obs[:, i, :], None if relu_masks is None else [m[i::2] for m in relu_masks])
     ml = ml.masked_fill(~masks[:, i, 0:5], float("-inf"))
     lp_move = torch.distributions.Categorical(logits=ml).log_prob(moves)
     kl = kl.squeeze().masked_fill(~masks[:, i, 5], float("-inf"))
@@ -152,16 +158,18 @@ def log_probs(actor, i, obs, act, masks):
     return lp_move + torch.log(p)
 
 
-def minibatch_grads(actor, critic, obs, act, old_lp, adv, rtg, masks, clip=0.2):
+def minibatch_grads(actor, critic, obs, act, old_lp, adv, rtg, masks, clip=0.2, patterns=None):
     """The two losses of PPO.py:62-80 and their gradients (before clip_grad_norm_
     and Adam).  Returns (actor_loss, critic_loss, {name: actor grad},
-    {name: critic grad}); works for fp32 or fp64 modules (inputs are cast)."""
+    {name: critic grad}); works for fp32 or fp64 modules (inputs are cast).
+    patterns: optional (actor relu masks, critic relu masks), see OActor.forward."""
     dt = next(actor.parameters()).dtype
     obs, adv, rtg, old_lp = (t.to(dt) for t in (obs, adv, rtg, old_lp))
-    V = critic(obs).squeeze()
+    pa, pc = patterns if patterns is not None else (None, None)
+    V = critic(obs, pc).squeeze()
     cur = 0
     for i in range(2):
-        cur = cur + log_probs(actor, i, obs, act, masks)
+        cur = cur + log_probs(actor, i, obs, act, masks, pa)
     ratio = torch.exp(cur - old_lp)
     aloss = -torch.mean(torch.min(ratio * adv, torch.clamp(ratio, 1 - clip, 1 + clip) * adv))
     closs = torch.nn.MSELoss()(V, rtg)
@@ -172,12 +180,14 @@ def minibatch_grads(actor, critic, obs, act, old_lp, adv, rtg, masks, clip=0.2):
 
 
 def minibatch_step(actor, critic, aopt, copt, obs, act, old_lp, adv, rtg, masks,
-                   clip=0.2, max_grad=0.5):
-    """One iteration of PPO.py:58-85.  Returns (actor_loss, critic_loss, gn_a, gn_c)."""
-    V = critic(obs).squeeze()
+                   clip=0.2, max_grad=0.5, patterns=None):
+    """One iteration of PPO.py:58-85.  Returns (actor_loss, critic_loss, gn_a, gn_c).
+    patterns: as minibatch_grads."""
+    pa, pc = patterns if patterns is not None else (None, None)
+    V = critic(obs, pc).squeeze()
     cur = 0
     for i in range(2):
-        cur = cur + log_probs(actor, i, obs, act, masks)
+        cur = cur + log_probs(actor, i, obs, act, masks, pa)
     ratio = torch.exp(cur - old_lp)
     s1 = ratio * adv
     s2 = torch.clamp(ratio, 1 - clip, 1 + clip) * adv

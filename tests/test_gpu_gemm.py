@@ -97,7 +97,8 @@ def test_gemm_forward_and_input_gradient(prec, M, N, K, algo):
     # the bits record y > 0 exactly
     w2 = torch.randn(48, N, device="cuda", generator=g) * 0.1  # the next layer's weight [out, in]
     dy = torch.randn(M, 48, device="cuda", generator=g) / M
-    ascale = 1.0 if prec == "x3" else float(2.0 ** 16)
+    # the product's fp16 dY scale (networks._grad_scale): 2^floor(log2 M) for gradients of a mean over M rows
+    ascale = 1.0 if prec == "x3" else float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
     if bits is None:  # the plain input-gradient form (the first layer's dx)
         dx = x3.gemm(dy, x3.pack(w2, trans=True, prec=prec), ascale=ascale)
         ref = dy.double() @ w2.double()
