@@ -149,7 +149,7 @@ def log_probs(actor, i, obs, act, masks, relu_masks=None):
     """PPO.get_log_probs (PPO.py:154-168).  relu_masks: the actor's patterns over
     the interleaved [2M] agent rows (row 2m + i), see OActor.forward."""
     moves, marks = act[:, i, 0], act[:, i, 1]
-    ml, kl = actor(obs[:, i, :], None if relu_masks is None else [m[i::2] for m in relu_masks])
+    ml, kl = actor(obs[:, i, :]) if relu_masks is None else actor(obs[:, i, :], [m[i::2] for m in relu_masks])
     ml = ml.masked_fill(~masks[:, i, 0:5], float("-inf"))
     lp_move = torch.distributions.Categorical(logits=ml).log_prob(moves)
     kl = kl.squeeze().masked_fill(~masks[:, i, 5], float("-inf"))
