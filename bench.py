@@ -46,10 +46,14 @@ def _cpu_model():
     return "unknown"
 
 
-def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4):
+def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4, max_steps=None, updates=5, full_batch=None):
     """One reference PPO.train() epoch (PPO.py:33-87) of the oracle's port: a
     single 10x10 maze, batch_size 15000 (whole episodes until more than that
-    are stored, PPO.py:108-141), then 5 x 5 minibatch updates of 3,000."""
+    are stored, PPO.py:108-141), then 5 x 5 minibatch updates of 3,000.
+    max_steps / updates < 5 bound the sample (the rollout's first max_steps
+    env-steps and `updates` of the 5 update passes); the epoch's time is then
+    extrapolated from the per-step and per-pass times, and the update runs on
+    full_batch (a full epoch's batch, (env_steps, tensors), from another run)."""
     from oracle.env import OracleEnv
     from oracle.ppo import CpuPPOPort
 
@@ -57,33 +61,46 @@ def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4):
     env = OracleEnv(1, default_size=(size, size), max_timestep=max_t, seeds=[0])
     port = CpuPPOPort(env, batch_size=batch_size, lr=lr)
     t0 = time.time()
-    steps, batch = port.get_batch()
+    steps, batch = port.get_batch(max_steps=max_steps)
     t_roll = time.time() - t0
+    if max_steps is not None:  # the update runs on a full epoch's batch
+        full, batch = full_batch
+        t_roll *= full / steps
+        steps = full
     t1 = time.time()
-    hist = port.update(batch)
-    t_upd = time.time() - t1
+    hist = port.update(batch, updates=updates)
+    t_upd = (time.time() - t1) * 5.0 / updates
+    n_mb = len(hist) * 5 // updates
     return dict(threads=threads, env_steps=steps, epoch_s=t_roll + t_upd, rollout_s=t_roll, update_s=t_upd,
                 env_steps_per_s=steps / (t_roll + t_upd), rollout_env_steps_per_s=steps / t_roll,
-                ppo_updates_per_s=len(hist) / t_upd, minibatch=batch_size // 5, minibatches=len(hist))
+                ppo_updates_per_s=n_mb / t_upd, minibatch=batch_size // 5, minibatches=n_mb,
+                sampled=("full epoch" if max_steps is None else
+                         f"first {max_steps} rollout env-steps and {updates} of 5 update passes, extrapolated"),
+                _batch=(steps, batch))
 
 
 def cpu_baseline():
     """BASELINE.md's CPU plan: one full train() epoch of
-    the CPU port at the box's CPU share of threads and at 1 thread.  The port's
-    environment is the C oracle (bit-exact to the reference's Python env, ~5x
-    faster than it: SURVEY §6), its networks / sampling / update are torch-CPU
-    fp32 like the reference's, so the figure OVERSTATES the reference's own
-    train() speed."""
+    the CPU port at the box's CPU share of threads and at 1 thread, and a
+    bounded sample of it at os.cpu_count() threads.  The port's environment is
+    the C oracle (bit-exact to the reference's Python env, ~5x faster than it:
+    SURVEY §6), its networks / sampling / update are torch-CPU fp32 like the
+    reference's, so the figure OVERSTATES the reference's own train() speed."""
     n_cpu = os.cpu_count() or 1
     share = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, n_cpu)
     runs = [_cpu_epoch(share), _cpu_epoch(1)]
+    if n_cpu > share:
+        runs.append(_cpu_epoch(n_cpu, max_steps=1500, updates=1, full_batch=runs[1]["_batch"]))
+    for r in runs:
+        del r["_batch"]
     best = max(runs, key=lambda r: r["env_steps_per_s"])  # the faster setting (1 thread usually: tiny per-step ops)
     return dict(value=best["env_steps_per_s"], unit="env-steps/s", cores=best["threads"], kind="port",
                 sample=f"one full PPO.train() epoch (batch_size 15000, lr 1.4e-4, 1 maze 10x10, max_timestep 1200) "
                        f"of oracle.ppo.CpuPPOPort: C-oracle env (bit-exact, ~5x faster than the reference's Python "
                        f"env) + torch-CPU fp32 actor/critic/Adam; {best['env_steps']} env-steps + "
                        f"{best['minibatches']} minibatch updates of {best['minibatch']} in {best['epoch_s']:.1f} s "
-                       f"at {best['threads']} thread(s) (the faster of {share} and 1)",
+                       f"at {best['threads']} thread(s) ({best['sampled']}; the fastest of "
+                       f"{', '.join(str(r['threads']) for r in runs)} threads)",
                 os_cpu_count=n_cpu, cpu_model=_cpu_model(), threads_used=[r["threads"] for r in runs],
                 runs=runs)
 
@@ -102,6 +119,9 @@ def main():
     ap.add_argument("--horizon", type=int, default=16, help="env-steps per maze per iteration")
     ap.add_argument("--max-t", type=int, default=1200, help="max_timestep (main.py:20)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="parity_mode=False: every feature embedding reads its own observation slice (not the "
+                         "reference's quirk Q1, under which the actor sees only obs[0:4])")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the rollout as a captured HIP graph (auto: on below 16,384 mazes per GPU, where the "
                          "per-step launches are host-bound); the env-step kernel's duration for the roofline then "
@@ -124,7 +144,7 @@ def main():
     batch_global = 5 * ((samples_local * world) // 5)
     graph = a.graph == "on" or (a.graph == "auto" and n < 16384)
     agent = PPO(2, epochs=1, batch_size=batch_global, lr=1.4e-4, n_envs=n, horizon=T, load=False, verbose=False,
-                save=False, dp=dp, sample_seed=12345, dtype=a.dtype, graph_rollout=graph,
+                save=False, dp=dp, sample_seed=12345, dtype=a.dtype, graph_rollout=graph, parity_mode=not a.no_parity,
                 env_config=dict(default_size=(a.size, a.size), max_timestep=a.max_t, seed_base=0))
 
     def iteration():
@@ -205,6 +225,7 @@ def main():
             "horizon": T, "global_batch": batch_global, "minibatch": batch_global // 5,
             "minibatch_steps_per_iter": minibatches_per_iter, "parallelism": f"dp{world}",
             "rollout": "HIP graph replay" if graph else "stream launches",
+            "parity_mode": not a.no_parity,
         },
         "ppo_updates_per_sec": minibatches_per_iter * a.steps / elapsed,
         "update_ms_per_iter": float(np.mean(upd_ms)),

@@ -290,11 +290,11 @@ class CpuPPOPort:
                  torch.as_tensor(B_val, dtype=torch.float32))
         return total, batch
 
-    def update(self, batch, n_minibatches=None):
+    def update(self, batch, updates=5):
         b_obs, b_act, b_lp, b_mask, b_adv, b_val = batch
         idx = np.arange(len(b_obs))
         np.random.shuffle(idx)
         bs = min(self.batch_size, len(b_obs))
         hist = update_epoch(self.actor, self.critic, self.aopt, self.copt, b_obs, b_act, b_lp,
-                            b_mask, b_adv, b_val, idx, bs)
+                            b_mask, b_adv, b_val, idx, bs, updates=updates)
         return hist
