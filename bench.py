@@ -79,6 +79,31 @@ def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4, max_st
                 _batch=(steps, batch))
 
 
+def _cpu_epoch_bounded(threads, full_batch, max_steps=1500, updates=1, timeout=60):
+    """_cpu_epoch at `threads` threads on a bounded sample, in a child process
+    with a time limit (torch at os.cpu_count() threads inside the box's CPU share
+    can be very slow on these tiny ops: a run past the limit is reported, not
+    waited for)."""
+    import subprocess
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "batch.pt")
+        torch.save({"steps": full_batch[0], "batch": list(full_batch[1])}, fb)
+        code = ("import json, sys, torch; sys.path[:0] = [%r, %r]; import bench; "
+                "fb = torch.load(%r, weights_only=True); "
+                "r = bench._cpu_epoch(%d, max_steps=%d, updates=%d, full_batch=(fb['steps'], tuple(fb['batch']))); "
+                "r.pop('_batch'); print(json.dumps(r))") % (REPO, os.path.join(REPO, "marl-maze_amd"), fb, threads,
+                                                             max_steps, updates)
+        try:
+            out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+            return json.loads(out.stdout.strip().splitlines()[-1])
+        except (subprocess.TimeoutExpired, ValueError, IndexError):
+            return dict(threads=threads, env_steps_per_s=0.0, timed_out_s=timeout,
+                        sampled=f"first {max_steps} rollout env-steps and {updates} of 5 update passes: did not "
+                                f"finish within {timeout} s")
+
+
 def cpu_baseline():
     """BASELINE.md's CPU plan: one full train() epoch of
     the CPU port at the box's CPU share of threads and at 1 thread, and a
@@ -88,11 +113,15 @@ def cpu_baseline():
     reference's, so the figure OVERSTATES the reference's own train() speed."""
     n_cpu = os.cpu_count() or 1
     share = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, n_cpu)
-    runs = [_cpu_epoch(share), _cpu_epoch(1)]
+    runs = []
+    for th in (share, 1):
+        print(f"cpu baseline: one train() epoch at {th} thread(s)", file=sys.stderr, flush=True)
+        runs.append(_cpu_epoch(th))
     if n_cpu > share:
-        runs.append(_cpu_epoch(n_cpu, max_steps=1500, updates=1, full_batch=runs[1]["_batch"]))
+        print(f"cpu baseline: bounded sample at os.cpu_count() = {n_cpu} threads", file=sys.stderr, flush=True)
+        runs.append(_cpu_epoch_bounded(n_cpu, runs[1]["_batch"]))
     for r in runs:
-        del r["_batch"]
+        r.pop("_batch", None)
     best = max(runs, key=lambda r: r["env_steps_per_s"])  # the faster setting (1 thread usually: tiny per-step ops)
     return dict(value=best["env_steps_per_s"], unit="env-steps/s", cores=best["threads"], kind="port",
                 sample=f"one full PPO.train() epoch (batch_size 15000, lr 1.4e-4, 1 maze 10x10, max_timestep 1200) "
