@@ -1244,8 +1244,13 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&c
     for (int c = 0; c < CT; c++) {
         if (c < ctn) {  // wave-uniform (a guard, not a break: the loop stays fully unrolled, acc in registers)
             bf16x8 bb[3];
+#ifdef BRES_NO_BREAD  // diagnostic builds only: B fragments from the A registers (no LDS reads; outputs wrong)
+#pragma unroll
+            for (int q = 0; q < np; q++) bb[q] = a[0][(q + c) % 3];
+#else
 #pragma unroll
             for (int q = 0; q < np; q++) bb[q] = bp[(c * np + q) * 64];
+#endif
 #pragma unroll
             for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb, acc[r][c]);
         }

@@ -1,6 +1,8 @@
 # Diagnostic / tuning builds of k_bres (csrc/x3mlp.hip), for tools/bench_gemm_ab.py through MARLMAZE_LIB:
 #   ROW0: every unit reads the same 32 A rows (L2-resident: no HBM latency on the A loads; outputs wrong);
 #   NOSPLIT: no A split (raw bits as fragments; outputs wrong);
+#   NOBREAD: no B fragment LDS reads (A registers reused as B; outputs wrong);
+# (tools/ab_build.py NAME -D... builds any combination; tools/ab_libs.py times builds in one process)
 #   W<n>_P<b>: <n> waves per workgroup, B fragments of the next column read ahead (b = 1) or not.
 set -e
 mkdir -p tools/_var
