@@ -284,6 +284,22 @@ int mm_gemm_nt_algo(int algo);
 long mm_gemm_wgrad_ws_len(int M, int N, int K);
 int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
                   float cscale, float* ws, float* dw, void* stream);
+/* The update's batched forms (one launch for what a backward would otherwise
+ * issue per layer; each result bit-identical to the single form):
+ * mm_gemm_tp_pack_multi: nseg <= 16 packs of one precision (mm_gemm_tp_pack's
+ * arguments per segment).
+ * mm_gemm_wgrad_partials: mm_gemm_wgrad without its final reduction: ws receives
+ * mm_gemm_wgrad_slices(prec, M, N, K) row-slice partials of [N, K], summed later
+ * by mm_wsum_multi with S = that count (M > 0). */
+typedef struct {
+    const float* X;
+    int R, C, ld, trans;
+    uint16_t* tp;
+} mm_pack_seg_t;
+int mm_gemm_tp_pack_multi(int prec, const mm_pack_seg_t* segs, int nseg, void* stream);
+int mm_gemm_wgrad_slices(int prec, int M, int N, int K);
+int mm_gemm_wgrad_partials(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
+                           int K, float cscale, float* ws, void* stream);
 
 /* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
  * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),
@@ -313,6 +329,25 @@ int mm_ppo_loss_bwd(const float* heads, const uint8_t* masks, const int8_t* acti
  * mm_losses_final: out[0] = -sum(ppo_partial) / M (the actor loss of
  * mm_ppo_loss), out[1] = sum(mse_partial) / M (the critic loss). */
 int mm_colsum(const float* x, long R, int N, float* part, int G, float* out, void* stream);
+/* mm_colsum_multi: nseg <= 16 column sums in two launches, segment k as
+ * mm_colsum(x, R, N, part, min(256, max(1, R / 8)), out) (bit-identical); ws:
+ * mm_colsum_multi_ws_len(segs, nseg) floats.  mm_wsum_multi: nseg <= 16 sums
+ * out [n] = sum over s < S of x[s n + e] in mm_gemm_wgrad's reduction order. */
+typedef struct {
+    const float* x;
+    long R;
+    int N;
+    float* out;
+} mm_colsum_seg_t;
+typedef struct {
+    const float* x;
+    long n;
+    int S;
+    float* out;
+} mm_wsum_seg_t;
+long mm_colsum_multi_ws_len(const mm_colsum_seg_t* segs, int nseg);
+int mm_colsum_multi(const mm_colsum_seg_t* segs, int nseg, float* ws, void* stream);
+int mm_wsum_multi(const mm_wsum_seg_t* segs, int nseg, void* stream);
 int mm_mse_loss_partials(int M);
 int mm_mse_loss(const float* v, const float* rtg, int M, float* dv, float* partial, void* stream);
 int mm_losses_final(const float* ppo_partial, int n_ppo, const float* mse_partial, int n_mse, int M, float* out,

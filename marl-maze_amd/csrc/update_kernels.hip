@@ -146,9 +146,156 @@ __global__ __launch_bounds__(256) void k_clip_adam(AdamSegs segs, const double* 
     }
 }
 
+// ---- several reductions in one launch (the update's bias gradients and weight-gradient partials
+// are reduced together at the end of a backward: per-launch latency, not bandwidth, is their cost) ----
+constexpr int kMaxMulti = 16;
+struct ColsumSegs {
+    mm_colsum_seg_t s[kMaxMulti];
+    int G[kMaxMulti];          // slabs
+    long rps[kMaxMulti];       // rows per slab
+    int blk1[kMaxMulti + 1];   // pass-1 workgroup prefix (G x column blocks)
+    int blk2[kMaxMulti + 1];   // pass-2 workgroup prefix (column blocks)
+    long woff[kMaxMulti];      // partials offset in ws (floats)
+    int nseg;
+};
+
+// one workgroup of k_colsum's body: rows r0 .. r1 of x [R, N], columns 64 cb .. (fixed order, as k_colsum)
+__device__ __forceinline__ void colsum_block(const float* __restrict__ x, long r0, long r1, int N, int cb,
+                                             float* __restrict__ out, float (*red)[64]) {
+    const int rl = threadIdx.x >> 6, c = cb * 64 + (threadIdx.x & 63);
+    float a0 = 0.f, a1 = 0.f;
+    if (c < N) {
+        long r = r0 + rl;
+#pragma unroll 4
+        for (; r + 4 < r1; r += 8) {
+            a0 += x[r * N + c];
+            a1 += x[(r + 4) * N + c];
+        }
+        if (r < r1) a0 += x[r * N + c];
+    }
+    red[rl][threadIdx.x & 63] = a0 + a1;
+    __syncthreads();
+    if (rl == 0 && c < N) {
+        const int k = threadIdx.x & 63;
+        out[c] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+    }
+}
+
+__device__ __forceinline__ int seg_of(const int* pre, int nseg, int b) {
+    int k = 0;
+    while (k + 1 < nseg && b >= pre[k + 1]) k++;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void k_colsum_multi1(ColsumSegs cs, float* __restrict__ ws) {
+    __shared__ float red[4][64];
+    const int k = seg_of(cs.blk1, cs.nseg, blockIdx.x);
+    const mm_colsum_seg_t& sg = cs.s[k];
+    const int b = blockIdx.x - cs.blk1[k], G = cs.G[k];
+    const int slab = b % G, cb = b / G;
+    const long r0 = slab * cs.rps[k], r1 = min(sg.R, r0 + cs.rps[k]);
+    colsum_block(sg.x, r0, r1, sg.N, cb, ws + cs.woff[k] + (long)slab * sg.N, red);
+}
+
+__global__ __launch_bounds__(256) void k_colsum_multi2(ColsumSegs cs, const float* __restrict__ ws) {
+    __shared__ float red[4][64];
+    const int k = seg_of(cs.blk2, cs.nseg, blockIdx.x);
+    const mm_colsum_seg_t& sg = cs.s[k];
+    colsum_block(ws + cs.woff[k], 0, cs.G[k], sg.N, blockIdx.x - cs.blk2[k], sg.out, red);
+}
+
+struct WsumSegs {
+    mm_wsum_seg_t s[kMaxMulti];
+    int blk[kMaxMulti + 1];  // workgroup prefix: ceil(n / 16) each
+    int nseg;
+};
+
+// out[e] = sum over s of x[s * n + e]: 16 groups of slices, each summed in order, then the groups in order
+// (the order of csrc/x3mlp.hip's k_wg_reduce: identical results)
+__global__ __launch_bounds__(256) void k_wsum_multi(WsumSegs ws) {
+    __shared__ float red[16][17];
+    const int k = seg_of(ws.blk, ws.nseg, blockIdx.x);
+    const mm_wsum_seg_t& sg = ws.s[k];
+    const int el = threadIdx.x & 15, g = threadIdx.x >> 4;
+    const long e = (blockIdx.x - ws.blk[k]) * 16L + el, n = sg.n;
+    const int S = sg.S, per = (S + 15) / 16, s0 = g * per, s1 = min(S, s0 + per);
+    float a = 0.f;
+    if (e < n) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = s0 + i < s1 ? sg.x[(long)(s0 + i) * n + e] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; i++) a += v[i];
+        for (int t = s0 + 16; t < s1; t++) a += sg.x[(long)t * n + e];  // S > 256
+    }
+    red[g][el] = a;
+    __syncthreads();
+    if (g == 0 && e < n) {
+        float t = red[0][el];
+#pragma unroll
+        for (int q = 1; q < 16; q++) t += red[q][el];
+        sg.out[e] = t;
+    }
+}
+
 }  // namespace mm
 
 using namespace mm;
+
+static bool colsum_plan(const mm_colsum_seg_t* segs, int nseg, ColsumSegs& cs, long& wlen) {
+    if (!segs || nseg <= 0 || nseg > kMaxMulti) return false;
+    cs.nseg = nseg;
+    cs.blk1[0] = cs.blk2[0] = 0;
+    wlen = 0;
+    for (int k = 0; k < nseg; k++) {
+        const mm_colsum_seg_t& g = segs[k];
+        if (!g.x || !g.out || g.R <= 0 || g.N <= 0) return false;
+        cs.s[k] = g;
+        long G = g.R / 8;  // slabs of >= 8 rows, at most 256 (as marlmaze.x3.colsum)
+        G = G < 1 ? 1 : G > 256 ? 256 : G;
+        const long rps = (g.R + G - 1) / G;
+        cs.G[k] = (int)((g.R + rps - 1) / rps);
+        cs.rps[k] = rps;
+        const int cb = (g.N + 63) / 64;
+        cs.blk1[k + 1] = cs.blk1[k] + cs.G[k] * cb;
+        cs.blk2[k + 1] = cs.blk2[k] + cb;
+        cs.woff[k] = wlen;
+        wlen += (long)cs.G[k] * g.N;
+    }
+    return true;
+}
+
+extern "C" long mm_colsum_multi_ws_len(const mm_colsum_seg_t* segs, int nseg) {
+    ColsumSegs cs;
+    long wlen;
+    return colsum_plan(segs, nseg, cs, wlen) ? wlen : MM_E_ARG;
+}
+
+extern "C" int mm_colsum_multi(const mm_colsum_seg_t* segs, int nseg, float* ws, void* stream) {
+    ColsumSegs cs;
+    long wlen;
+    if (!colsum_plan(segs, nseg, cs, wlen) || !ws) return MM_E_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_colsum_multi1, dim3(cs.blk1[nseg]), dim3(256), 0, st, cs, ws);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(k_colsum_multi2, dim3(cs.blk2[nseg]), dim3(256), 0, st, cs, (const float*)ws);
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_wsum_multi(const mm_wsum_seg_t* segs, int nseg, void* stream) {
+    if (!segs || nseg <= 0 || nseg > kMaxMulti) return MM_E_ARG;
+    WsumSegs w;
+    w.nseg = nseg;
+    w.blk[0] = 0;
+    for (int k = 0; k < nseg; k++) {
+        if (!segs[k].x || !segs[k].out || segs[k].S <= 0 || segs[k].n <= 0) return MM_E_ARG;
+        w.s[k] = segs[k];
+        w.blk[k + 1] = w.blk[k] + (int)((segs[k].n + 15) / 16);
+    }
+    hipLaunchKernelGGL(k_wsum_multi, dim3(w.blk[nseg]), dim3(256), 0, (hipStream_t)stream, w);
+    return (int)hipGetLastError();
+}
 
 extern "C" int mm_colsum(const float* x, long R, int N, float* part, int G, float* out, void* stream) {
     if (!x || !out || R <= 0 || N <= 0 || G <= 0 || (G > 1 && !part)) return MM_E_ARG;

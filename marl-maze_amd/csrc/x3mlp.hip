@@ -163,6 +163,39 @@ __global__ __launch_bounds__(256) void k_tp_pack(const float* __restrict__ X, in
     }
 }
 
+// several packs in one launch (the update packs every weight of a network before its backward):
+// the pieces of all segments laid end to end, each piece packed as by k_tp_pack
+constexpr int kMaxPackSegs = 16;
+struct PackSegs {
+    mm_pack_seg_t s[kMaxPackSegs];
+    long pre[kMaxPackSegs + 1];  // piece prefix
+    int nks[kMaxPackSegs];
+    int nseg;
+};
+
+template <int P>
+__global__ __launch_bounds__(256) void k_tp_pack_multi(PackSegs ps) {
+    const long total = ps.pre[ps.nseg];
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        int k = 0;
+        while (k + 1 < ps.nseg && t >= ps.pre[k + 1]) k++;
+        const mm_pack_seg_t& g = ps.s[k];
+        const long e = t - ps.pre[k];
+        const int l = (int)(e & 63);
+        const long blk = e >> 6;
+        const int nks = ps.nks[k], ks = (int)(blk % nks), rt = (int)(blk / nks);
+        const int row = 16 * rt + (l & 15), c = l >> 4;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int col = 32 * ks + kcol(c, j);
+            v[j] = (row < g.R && col < g.C) ? (g.trans ? g.X[(size_t)col * g.ld + row] : g.X[(size_t)row * g.ld + col])
+                                            : 0.f;
+        }
+        store_piece<P>(v, 1.f, reinterpret_cast<uint4*>(g.tp + blk * Prec<P>::kBlk) + l);
+    }
+}
+
 #ifndef X3_WAVES
 #define X3_WAVES 16
 #endif
@@ -1446,6 +1479,29 @@ extern "C" int mm_gemm_tp_pack(int prec, const float* X, int R, int C, int ld, i
     return (int)hipGetLastError();
 }
 
+extern "C" int mm_gemm_tp_pack_multi(int prec, const mm_pack_seg_t* segs, int nseg, void* stream) {
+    if (!segs || nseg <= 0 || nseg > kMaxPackSegs) return MM_E_ARG;
+    PackSegs ps;
+    ps.nseg = nseg;
+    ps.pre[0] = 0;
+    for (int k = 0; k < nseg; k++) {
+        const mm_pack_seg_t& g = segs[k];
+        if (!g.X || !g.tp || g.R <= 0 || g.C <= 0 || g.ld < (g.trans ? g.R : g.C) || ((uintptr_t)g.tp & 15))
+            return MM_E_ARG;
+        ps.s[k] = g;
+        ps.nks[k] = rup(g.C, 32) / 32;
+        ps.pre[k + 1] = ps.pre[k] + (long)(rup(g.R, kRowPad) / 16) * ps.nks[k] * 64;
+    }
+    const int grid = (int)std::min<long>((ps.pre[nseg] + 255) / 256, 256L * 64);
+    if (prec == MM_PREC_X3)
+        hipLaunchKernelGGL(k_tp_pack_multi<P_X3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ps);
+    else if (prec == MM_PREC_F16)
+        hipLaunchKernelGGL(k_tp_pack_multi<P_F16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ps);
+    else
+        return MM_E_ARG;
+    return (int)hipGetLastError();
+}
+
 extern "C" int mm_x3_tp_pack(const float* X, int R, int C, int ld, int trans, uint16_t* tp, void* stream) {
     return mm_gemm_tp_pack(MM_PREC_X3, X, R, C, ld, trans, tp, stream);
 }
@@ -1849,13 +1905,13 @@ static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int ldd
                               : launch_rect_p<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
 }
 
-extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
-                             int K, float cscale, float* ws, float* dw, void* stream) {
-    if (!dw || M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
+static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
+                      float cscale, float* ws, float* dw, void* stream) {
+    if (M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
     if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (dscale != 1.f || cscale != 1.f)) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
-    if (M == 0) return (int)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)N * K, s);  // (empty inputs: no pointers)
+    if (M == 0) return dw ? (int)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)N * K, s) : MM_E_ARG;
     if (!dy || !x || !ws) return MM_E_ARG;
     const WgPlan p = wg_plan(prec, M, N, K);
     if (!p.TPW) return MM_E_ARG;
@@ -1864,7 +1920,25 @@ extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, 
                                        : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
     if (e) return e;
     const long n = (long)N * K;
-
+    if (!dw) return 0;  // mm_gemm_wgrad_partials: the caller reduces (mm_wsum_multi)
     hipLaunchKernelGGL(k_wg_reduce, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, s, ws, p.nslices, n, dw);
     return (int)hipGetLastError();
+}
+
+extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
+                             int K, float cscale, float* ws, float* dw, void* stream) {
+    if (!dw) return MM_E_ARG;
+    return gemm_wgrad(prec, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, dw, stream);
+}
+
+extern "C" int mm_gemm_wgrad_slices(int prec, int M, int N, int K) {
+    if (M <= 0 || N <= 0 || K <= 0 || (prec != MM_PREC_X3 && prec != MM_PREC_F16)) return MM_E_ARG;
+    const WgPlan p = wg_plan(prec, M, N, K);
+    return p.TPW ? p.nslices : MM_E_ARG;
+}
+
+extern "C" int mm_gemm_wgrad_partials(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
+                                      int N, int K, float cscale, float* ws, void* stream) {
+    if (M <= 0) return MM_E_ARG;
+    return gemm_wgrad(prec, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, nullptr, stream);
 }

@@ -434,16 +434,21 @@ class PPO:
         M = obs.shape[0]
         a8 = (act if act.dtype == torch.int8 else act.to(torch.int8)).contiguous()
         mk = _u8(masks)
-        V, csaved = self.critic.train_forward(obs.reshape(M, -1))
-        mse_part, dv = update.mse_loss(V, rtg)
-        heads, asaved = self.actor.train_forward(obs.reshape(2 * M, 65))
-        coef, ppo_part = _ppo_loss_fwd(heads, mk, a8, old_logp, adv, self.clip)
-        dz = _ppo_loss_bwd(heads, mk, a8, coef, self._one)
-        if out is None:
-            out = torch.empty(2, dtype=torch.float32, device=obs.device)
-        update.losses_final(ppo_part, mse_part, M, out)
-        self.actor.train_backward(asaved, dz)
-        self.critic.train_backward(csaved, dv)
+        with x3.cached_packs():
+            # every weight pack of both networks' forward and backward in one launch per precision, and
+            # the backwards' bias-gradient and weight-gradient reductions together at their end
+            x3.pack_many(self.critic.pack_specs() + self.actor.pack_specs())
+            V, csaved = self.critic.train_forward(obs.reshape(M, -1))
+            mse_part, dv = update.mse_loss(V, rtg)
+            heads, asaved = self.actor.train_forward(obs.reshape(2 * M, 65))
+            coef, ppo_part = _ppo_loss_fwd(heads, mk, a8, old_logp, adv, self.clip)
+            dz = _ppo_loss_bwd(heads, mk, a8, coef, self._one)
+            if out is None:
+                out = torch.empty(2, dtype=torch.float32, device=obs.device)
+            update.losses_final(ppo_part, mse_part, M, out)
+            with x3.deferred():
+                self.actor.train_backward(asaved, dz)
+                self.critic.train_backward(csaved, dv)
         return out[0], out[1]
 
     def _minibatch_grads_host(self, obs, act, old_logp, adv, rtg, masks):

@@ -42,8 +42,9 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
            "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
-           "mm_clip_adam_ws_len", "mm_clip_adam")
-VERSION = 300  # mm_version() this binding is written for
+           "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
+           "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi")
+VERSION = 301  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
@@ -73,6 +74,22 @@ class AdamSeg(ctypes.Structure):
         ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_long), ("max_norm", ctypes.c_float),
         ("step_size", ctypes.c_float), ("bc2_sqrt", ctypes.c_float), ("grad_scale", ctypes.c_float),
     ]
+
+
+class PackSeg(ctypes.Structure):
+    """mirror of mm_pack_seg_t"""
+    _fields_ = [("X", ctypes.c_void_p), ("R", ctypes.c_int), ("C", ctypes.c_int), ("ld", ctypes.c_int),
+                ("trans", ctypes.c_int), ("tp", ctypes.c_void_p)]
+
+
+class ColsumSeg(ctypes.Structure):
+    """mirror of mm_colsum_seg_t"""
+    _fields_ = [("x", ctypes.c_void_p), ("R", ctypes.c_long), ("N", ctypes.c_int), ("out", ctypes.c_void_p)]
+
+
+class WsumSeg(ctypes.Structure):
+    """mirror of mm_wsum_seg_t"""
+    _fields_ = [("x", ctypes.c_void_p), ("n", ctypes.c_long), ("S", ctypes.c_int), ("out", ctypes.c_void_p)]
 
 
 _LIB = None
@@ -160,6 +177,18 @@ def lib():
         L.mm_gemm_wgrad_ws_len.restype = ctypes.c_long
         L.mm_gemm_wgrad.argtypes = [i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P, P]
         L.mm_gemm_wgrad.restype = i32
+        L.mm_gemm_tp_pack_multi.argtypes = [i32, ctypes.POINTER(PackSeg), i32, P]
+        L.mm_gemm_tp_pack_multi.restype = i32
+        L.mm_gemm_wgrad_slices.argtypes = [i32, i32, i32, i32]
+        L.mm_gemm_wgrad_slices.restype = i32
+        L.mm_gemm_wgrad_partials.argtypes = [i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P]
+        L.mm_gemm_wgrad_partials.restype = i32
+        L.mm_colsum_multi_ws_len.argtypes = [ctypes.POINTER(ColsumSeg), i32]
+        L.mm_colsum_multi_ws_len.restype = ctypes.c_long
+        L.mm_colsum_multi.argtypes = [ctypes.POINTER(ColsumSeg), i32, P, P]
+        L.mm_colsum_multi.restype = i32
+        L.mm_wsum_multi.argtypes = [ctypes.POINTER(WsumSeg), i32, P]
+        L.mm_wsum_multi.restype = i32
         L.mm_x3_mbits_len.argtypes = [i32]
         L.mm_x3_mbits_len.restype = ctypes.c_long
         L.mm_x3_nt_f32a.restype = i32

@@ -231,12 +231,11 @@ def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None):
         o_w, o_b = (outs[2 * l], outs[2 * l + 1]) if outs is not None else (None, None)
         grads[2 * l] = _wgrad(dy, hs[l], prec, out=o_w)
         grads[2 * l + 1] = x3.colsum(dy if cs is None else cs, out=o_b)
-        wt = x3.pack(ws[l], trans=True, prec=prec)
         if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0): the ReLU bits of layer l-1's forward
             cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
-            dy = x3.gemm(dy, wt, mbits_in=ctx_bits[l - 1], colsum=cs, ascale=s)
+            dy = x3.gemm(dy, x3.pack(ws[l], trans=True, prec=prec), mbits_in=ctx_bits[l - 1], colsum=cs, ascale=s)
         elif need_dx:
-            dx = x3.gemm(dy, wt, ascale=s)
+            dx = x3.gemm(dy, x3.pack(ws[l], trans=True, prec=prec), ascale=s)
     return dx, grads
 
 
@@ -391,10 +390,25 @@ class Actor(nn.Module):
 
     def heads(self):
         """[move_head; mark_head] as one [6, K] weight and [6] bias (views when the
-        parameters are laid out adjacently, else concatenated copies)."""
+        parameters are laid out adjacently -- the same view objects while the
+        parameters stay where they are, so packs of them are cached -- else
+        concatenated copies)."""
         mw, kw, mb, kb = self.move_head.weight, self.mark_head.weight, self.move_head.bias, self.mark_head.bias
+        key = tuple((t.data_ptr(), t.shape) for t in (mw, kw, mb, kb))
+        hit = self.__dict__.get("_heads_view")
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
         w, b = self._adjacent(mw, kw), self._adjacent(mb, kb)
+        if w is not None and b is not None:
+            self.__dict__["_heads_view"] = (key, w, b)
+            return w, b
         return (w if w is not None else torch.cat([mw, kw], 0), b if b is not None else torch.cat([mb, kb], 0))
+
+    def pack_specs(self):
+        """The weight packs (x3.pack_many specs) of one train_forward + train_backward."""
+        ws = [lin.weight for lin in self.layers]
+        return ([(w, False, self.gemm_prec) for w in ws] + [(self.heads()[0], False, "x3")]
+                + [(w, True, self.gemm_prec) for w in ws])
 
     def forward(self, x):
         heads = self.logits(x)
@@ -582,6 +596,11 @@ class Critic(nn.Module):
         assert x.is_cuda and self._engine(x)
         v, hs, bits = _critic_fwd(x, self._params(), self.gemm_prec, True)
         return v, (hs, bits)
+
+    def pack_specs(self):
+        """The weight packs (x3.pack_many specs) of one train_forward + train_backward."""
+        ws = [lin.weight for lin in self.layers]
+        return [(w, False, self.gemm_prec) for w in ws] + [(w, True, self.gemm_prec) for w in ws[1:-1]]
 
     def train_backward(self, saved, dv):
         """Every parameter's gradient for d loss / d V (dv [M, 1]) into .grad."""

@@ -59,31 +59,111 @@ class cached_packs:
         return False
 
 
+def _cache_get(x, key):
+    ent = _PACK_CACHE.get(id(x), {}).get(key)
+    if (ent is not None and ent[0]() is x and ent[1] == x.data_ptr() and ent[2] == x._version
+            and ent[3] == _GENERATION[0]):
+        return ent[4]
+    return None
+
+
+def _cache_put(x, key, res):
+    if len(_PACK_CACHE) > 256:  # drop entries of tensors that are gone
+        for k in [k for k, v in _PACK_CACHE.items() if all(e[0]() is None for e in v.values())]:
+            del _PACK_CACHE[k]
+    d = _PACK_CACHE.get(id(x))
+    if d is None or any(e[0]() is not x for e in d.values()):  # a new tensor at a reused id
+        d = _PACK_CACHE[id(x)] = {}
+    d[key] = (weakref.ref(x), x.data_ptr(), x._version, _GENERATION[0], res)
+
+
+def _pack_shape(x, trans):
+    assert x.dtype == torch.float32 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
+    R, C = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
+    return R, C, (bool(trans), tuple(x.shape), x.stride(0))
+
+
 def pack(x, out=None, trans=False, prec="x3"):
     """fp32 [R, C] (or its transpose when trans=True, reading x as [C, R]) -> TP (reused inside a
     ``cached_packs()`` scope while the tensor is unchanged)."""
-    assert x.dtype == torch.float32 and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
-    R, C = (x.shape[1], x.shape[0]) if trans else (x.shape[0], x.shape[1])
-    key = (bool(trans), prec, tuple(x.shape), x.stride(0))
+    R, C, key = _pack_shape(x, trans)
+    key = (prec,) + key
     cache = out is None and _CACHE_DEPTH[0] > 0
     if cache:
-        ent = _PACK_CACHE.get(id(x), {}).get(key)
-        if (ent is not None and ent[0]() is x and ent[1] == x.data_ptr() and ent[2] == x._version
-                and ent[3] == _GENERATION[0]):
-            return ent[4]
+        hit = _cache_get(x, key)
+        if hit is not None:
+            return hit
     res = out if out is not None else TP(R, C, x.device, prec=prec)
     assert (res.R, res.C, res.prec) == (R, C, prec)
     _lib.check(_lib.lib().mm_gemm_tp_pack(PRECS[prec], _lib.ptr(x), R, C, x.stride(0), int(trans), res.ptr(),
                                           _lib.stream_ptr()), "mm_gemm_tp_pack")
     if cache:
-        if len(_PACK_CACHE) > 256:  # drop entries of tensors that are gone
-            for k in [k for k, v in _PACK_CACHE.items() if all(e[0]() is None for e in v.values())]:
-                del _PACK_CACHE[k]
-        d = _PACK_CACHE.get(id(x))
-        if d is None or any(e[0]() is not x for e in d.values()):  # a new tensor at a reused id
-            d = _PACK_CACHE[id(x)] = {}
-        d[key] = (weakref.ref(x), x.data_ptr(), x._version, _GENERATION[0], res)
+        _cache_put(x, key, res)
     return res
+
+
+def pack_many(specs):
+    """Pack several weights at once -- specs: (x, trans, prec) -- in one launch per precision
+    (mm_gemm_tp_pack_multi, <= 16 a launch) into the ``cached_packs()`` cache, so that the pack() calls
+    of a forward and backward that follow find them.  Tensors already cached are skipped.  Returns the
+    TPs in spec order."""
+    assert _CACHE_DEPTH[0] > 0, "pack_many fills the cache of a cached_packs() scope"
+    res, todo = [], {}
+    for x, trans, prec in specs:
+        R, C, key = _pack_shape(x, trans)
+        key = (prec,) + key
+        tp = _cache_get(x, key)
+        if tp is None:
+            tp = TP(R, C, x.device, prec=prec)
+            todo.setdefault(prec, []).append(_lib.PackSeg(_lib.ptr(x), R, C, x.stride(0), int(trans), tp.ptr()))
+            _cache_put(x, key, tp)
+        res.append(tp)
+    L = _lib.lib()
+    for prec, segs in todo.items():
+        for i in range(0, len(segs), 16):
+            chunk = segs[i:i + 16]
+            arr = (_lib.PackSeg * len(chunk))(*chunk)
+            _lib.check(L.mm_gemm_tp_pack_multi(PRECS[prec], arr, len(chunk), _lib.stream_ptr()),
+                       "mm_gemm_tp_pack_multi")
+    return res
+
+
+# Reductions deferred to the end of a backward: inside a ``deferred()`` scope, colsum(x, out) and
+# wgrad(..., out) launch their per-slab / per-slice partials only, and the final sums of all of them run
+# together when the scope ends (mm_colsum_multi / mm_wsum_multi: two + one launches for up to 16 each,
+# bit-identical to the per-call forms).  The outputs are valid after the scope.
+_DEFER = []
+
+
+class deferred:
+    def __enter__(self):
+        self.cols, self.sums, self.keep = [], [], []
+        _DEFER.append(self)
+        return self
+
+    def __exit__(self, exc_type, *exc):
+        _DEFER.remove(self)
+        if exc_type is None:
+            self.flush()
+        return False
+
+    def flush(self):
+        L, st = _lib.lib(), _lib.stream_ptr()
+        for i in range(0, len(self.cols), 16):
+            chunk = self.cols[i:i + 16]
+            arr = (_lib.ColsumSeg * len(chunk))(*chunk)
+            n = L.mm_colsum_multi_ws_len(arr, len(chunk))
+            _lib.check(n if n < 0 else 0, "mm_colsum_multi_ws_len")
+            dev = self.keep[0].device
+            ws = torch.empty(max(1, n), dtype=torch.float32, device=dev)
+            self.keep.append(ws)
+            _lib.check(L.mm_colsum_multi(arr, len(chunk), _lib.ptr(ws), st), "mm_colsum_multi")
+        for i in range(0, len(self.sums), 16):
+            chunk = self.sums[i:i + 16]
+            arr = (_lib.WsumSeg * len(chunk))(*chunk)
+            _lib.check(L.mm_wsum_multi(arr, len(chunk), st), "mm_wsum_multi")
+        # the scratch is freed to torch's caching allocator on this stream: reuse is stream-ordered
+        self.cols, self.sums, self.keep = [], [], []
 
 
 def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None, ascale=1.0, out=None):
@@ -113,13 +193,27 @@ def set_algo(name):
 
 def wgrad(dy, x, prec="x3", dscale=1.0, out=None):
     """dW [N, K] = dY^T X summed over the M rows (mm_gemm_wgrad), dY [M, N] and
-    X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two)."""
+    X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two).
+    Inside a ``deferred()`` scope with ``out`` given, the row-slice partials'
+    sum runs when the scope ends."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dy.stride(1) == 1 and x.stride(1) == 1
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
     L = _lib.lib()
+    if _DEFER and M > 0:
+        assert out.is_contiguous()
+        S = L.mm_gemm_wgrad_slices(PRECS[prec], M, N, K)
+        _lib.check(S if S < 0 else 0, "mm_gemm_wgrad_slices")
+        ws = torch.empty(S * N * K, dtype=torch.float32, device=dy.device)
+        _lib.check(L.mm_gemm_wgrad_partials(PRECS[prec], _lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x),
+                                            x.stride(0), M, N, K, 1.0 / float(dscale), _lib.ptr(ws),
+                                            _lib.stream_ptr()), "mm_gemm_wgrad_partials")
+        d = _DEFER[-1]
+        d.sums.append(_lib.WsumSeg(_lib.ptr(ws), N * K, S, _lib.ptr(out)))
+        d.keep += [ws, out]
+        return out
     ws = torch.empty(max(1, L.mm_gemm_wgrad_ws_len(M, N, K)), dtype=torch.float32, device=dy.device)
     _lib.check(L.mm_gemm_wgrad(PRECS[prec], _lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M,
                                N, K, 1.0 / float(dscale), _lib.ptr(ws), _lib.ptr(out), _lib.stream_ptr()),
@@ -170,13 +264,20 @@ def colsum_buf(M, N, device):
 
 def colsum(x, out=None, slabs=256):
     """x [R, N] f32 -> column sums [N] (mm_colsum: two passes in a fixed order) -- the bias gradients,
-    from the GEMM epilogues' per-tile sums or straight from dY."""
+    from the GEMM epilogues' per-tile sums or straight from dY.  Inside a ``deferred()`` scope with
+    ``out`` given (and the default slabs), the sum runs when the scope ends."""
     x = x.contiguous()
     R, N = x.shape
     if out is None:
         out = torch.empty(N, dtype=torch.float32, device=x.device)
     if R == 0:
         return out.zero_()
+    if _DEFER and slabs == 256:
+        assert out.is_contiguous() and out.numel() == N
+        d = _DEFER[-1]
+        d.cols.append(_lib.ColsumSeg(_lib.ptr(x), int(R), int(N), _lib.ptr(out)))
+        d.keep += [x, out]
+        return out
     G = max(1, min(int(slabs), int(R) // 8))  # slabs of >= 8 rows
     part = torch.empty((G, N), dtype=torch.float32, device=x.device) if G > 1 else None
     _lib.check(_lib.lib().mm_colsum(_lib.ptr(x), int(R), int(N), _lib.ptr(part), G, _lib.ptr(out),

@@ -127,3 +127,57 @@ def test_flat_adam_state_dict_round_trip():
     update.clip_adam([oa], 0.0)
     for p, q in zip(a.parameters(), ra.parameters()):
         assert (p.cpu() - q).abs().max().item() <= 1e-6 * q.abs().max().item()
+
+
+# ---- the batched forms (one launch for a backward's packs / reductions): bit-identical to the single ----
+
+def test_colsum_deferred_bit_identical():
+    """x3.deferred(): 20 column sums (two mm_colsum_multi launches of <= 16) == mm_colsum each."""
+    torch.manual_seed(5)
+    shapes = [(1, 5), (7, 264), (26215, 264), (13108, 130), (1000, 1), (3000, 6), (8, 64), (15, 3)] * 2
+    shapes += [(209715, 64), (64, 272), (17, 17), (4096, 6)]
+    xs = [torch.randn(R, N, device="cuda") for R, N in shapes]
+    ref = [x3.colsum(x) for x in xs]
+    outs = [torch.full((x.shape[1],), float("nan"), device="cuda") for x in xs]
+    with x3.deferred():
+        for x, o in zip(xs, outs):
+            x3.colsum(x, out=o)
+    for r, o in zip(ref, outs):
+        assert torch.equal(r, o)
+
+
+@pytest.mark.parametrize("prec", ["x3", "f16"])
+def test_wgrad_deferred_bit_identical(prec):
+    """x3.deferred(): weight gradients as partials + one mm_wsum_multi == mm_gemm_wgrad."""
+    torch.manual_seed(6)
+    shapes = [(3000, 264, 264), (26215, 64, 130), (5, 6, 264), (13108, 1, 64), (4096, 264, 460), (33, 64, 64)]
+    cases = []
+    for M, N, K in shapes:
+        s = 2.0 ** 10 if prec == "f16" else 1.0
+        cases.append((torch.randn(M, N, device="cuda") / M, torch.randn(M, K, device="cuda"), s))
+    ref = [x3.wgrad(dy, x, prec=prec, dscale=s) for dy, x, s in cases]
+    outs = [torch.full((dy.shape[1], x.shape[1]), float("nan"), device="cuda") for dy, x, _ in cases]
+    with x3.deferred():
+        for (dy, x, s), o in zip(cases, outs):
+            x3.wgrad(dy, x, prec=prec, dscale=s, out=o)
+        assert all(torch.isnan(o).all() for o in outs)  # not reduced yet
+    for r, o in zip(ref, outs):
+        assert torch.equal(r, o)
+
+
+def test_pack_many_equals_pack():
+    """pack_many (mm_gemm_tp_pack_multi, 18 packs over two precisions) writes the same TP planes as
+    pack, and the pack() calls that follow in the scope return those TPs."""
+    torch.manual_seed(7)
+    mats = [torch.randn(r, c, device="cuda") for r, c in [(264, 460), (264, 264), (6, 264), (1, 64), (64, 130),
+                                                             (64, 64), (272, 272), (3, 5), (300, 33)]]
+    specs = [(m, t, p) for m in mats for t in (False, True) for p in ("x3",)]
+    specs += [(mats[0], False, "f16"), (mats[4], True, "f16")]
+    with x3.cached_packs():
+        tps = x3.pack_many(specs)
+        for (m, t, p), tp in zip(specs, tps):
+            assert x3.pack(m, trans=t, prec=p) is tp
+    for (m, t, p), tp in zip(specs, tps):
+        ref = x3.pack(m, trans=t, prec=p)
+        assert (ref.R, ref.C, ref.prec) == (tp.R, tp.C, tp.prec)
+        assert torch.equal(ref.buf, tp.buf)
