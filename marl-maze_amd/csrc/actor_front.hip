@@ -741,338 +741,360 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
 }
 
 // ---------------------------------------------------------------------------
-// backward on the MFMA (k_front_bwd_mfma): the per-sample attention products
-// run as 16x16x16 bf16 MFMA tiles with the exact three-way split (six products
-// per fp32 product, as csrc/x3mlp.hip), tokens padded 23 -> 32, d_k 10 -> 16,
-// d_v 20 -> 32.  One wavefront per sample (two samples per wave per
-// iteration).  Accumulator tiles feed the next products directly: a C tile
-// (lane l holds rows 4 (l >> 4) + g, column l & 15) is the B operand of a
-// 16x16x16 MFMA whose k runs over its rows, and its transpose is an A
-// operand -- so
-//   S   = Q K^T          (A: Q rows, B: K rows; computed in-lane)
-//   dP  = dctx V^T       (A: dctx rows from dh, B: V rows in-lane)
-//   dV^T = dctx^T P      (B = the P tiles themselves)
-//   dK^T = Q^T dS        (B = the dS tiles)
-//   dQ  = dS K           (A = dS re-read through a 4-KiB LDS transpose)
-// and every q/k/v operand value is formed in the lane that needs it from the
-// folded maps (4 FMAs each).  Softmax and dS = P (dP - rowsum(P dP)) / sqrt(10)
-// act on the C tiles (row reductions across 16 lanes).  The per-token
-// gradients g = [dq | dk | dv], dctx and x go to the same LDS rows as in
-// k_front_bwd, whose E/F accumulation phase follows unchanged.
-//
-// Measured (tools/bench_front.py, 419,430 rows; tools/pmc_front.sh): 2.70 ms
-// against k_front_bwd's 1.85 ms, so it is not the default.  It executes 2,196
-// VALU instructions per sample against the VALU kernel's 1,213: the exact
-// three-way split of every operand value (~700 per sample) and the 32 x 32
-// padding of the 23 x 23 attention (softmax and dS on 1,024 entries instead
-// of 529) cost more VALU than the 168 MFMAs per sample save.
-typedef __attribute__((ext_vector_type(4))) short s16x4;
+// backward on the fp32 MFMA (k_front_bwd_mfma)
+// ---------------------------------------------------------------------------
+// The per-sample attention products run as v_mfma_f32_16x16x4_f32 tiles
+// (fp32 operands, an exact fmaf chain per output: no operand split), tokens
+// padded 23 -> 32.  One wavefront per sample, two samples per wave per
+// iteration.  The attention is held TRANSPOSED, S^T [j][i] (C tile: lane l
+// holds rows j = 4 (l >> 4) + g, column i = l & 15), so a softmax row (over j
+// for query i) is 8 values in the lane plus the 4 lane groups of 16 (two
+// permlane swaps).  Products (k = the summed index):
+//   S^T  = K Q^T          k = a: A = k rows, B = q rows      (QKV in LDS)
+//   dP^T = V dctx^T       k = c: A = v rows (LDS), B = dctx (dh)
+//   dQ^T = K^T dS^T       k = j: B = the dS^T C tiles themselves (register g of
+//                         a tile is the B operand whose k-lane q4 is row 4 q4 + g)
+//   dV   = P^T dctx       k = i: A = P^T rows through a 4.5-KiB LDS transpose
+//   dK   = dS^T Q         k = i: A = dS^T rows through the same buffer
+// Phase 1 (one lane per token, both samples of the wave at once) forms every
+// token's q|k|v once from the folded maps into LDS (QKV [32][44]: q at 0, k at
+// 12, v at 24, zero pads and padding tokens), so operands load as aligned
+// float4 (one per 4 MFMAs) or from a zero pad (no exec-masked loads); the
+// region is reused for the transposes once the operands are in registers, then
+// for the reduction operands G = [dq | dk | dv], dctx and x of k_front_bwd,
+// whose E/F accumulation phase follows unchanged.  5.9 KB of LDS per sample,
+// 47 KB per 8-sample workgroup: three workgroups per CU.  The softmax runs on
+// exp2 / rcp (v_exp_f32, v_rcp_f32: ~1 ulp; the reference's
+// exp(x / sqrt(10) - max) * (1 / sum) within ~3e-7 relative).
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
-// 4 fp32 -> three bf16 planes (x = hi + mid + lo exactly), hardware RNE conversions
-__device__ __forceinline__ void split4(const float* v, s16x4 (&p)[3]) {
-    typedef __attribute__((ext_vector_type(2))) __bf16 bf2;
-    typedef __attribute__((ext_vector_type(2))) float f2;
-    uint32_t h[2], m[2], l[2];
+constexpr int kQp = 44;                      // QKV row pitch (floats): [32 tokens][44]
+constexpr int kQO = 0, kKO = 12, kVO = 24;   // q | 0 0 | k | 0 0 | v
+constexpr int kTp = 36;                      // transpose buffer T [j][i], pitch 36 (j-major)
+// reduction operands G [23][40] | dctx [23][20] | x [23][4]: 0, 936, 1396 (dctx 16 words past G's end: the E/F
+// phase's 16-byte reads of a token's G and dctx rows fall in different LDS banks)
+constexpr int kMG = 0, kMD = kTok * kQkv + 16, kMX = kMD + kTok * kEmb;
+constexpr int kMSample = kMX + kTok * kPin;  // 1,488 floats per sample
+static_assert(32 * kQp <= kMSample && 32 * kTp <= kMSample, "QKV and T live in the sample's region");
+static_assert(kTok * kTp <= kMD, "the transpose rows j < 23 stay below dctx");
+constexpr float kLog2eRsqrtKq = 1.44269504088896341f * 0.316227766016838f;  // log2(e) / sqrt(10)
+
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float f4at(const float4& v, int e) {
+    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+}
+
+// sum / max over the four 16-lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48): the same value in every lane
+// (each swap pairs the lower group's value with the upper's, in that order)
+__device__ __forceinline__ float xq_sum(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+__device__ __forceinline__ float xq_max(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+#ifndef FRONT_MFMA_PREFETCH
+#define FRONT_MFMA_PREFETCH 0  // 1: global operands loaded one sample / iteration ahead (16 spilled VGPRs: slower)
+#endif
+
+// dP^T's B operand of one sample (dh row grow): rows 16 t + c16 (zero past token 22), columns 4 q4 .. 4 q4 + 3
+// and 16 + q4
+__device__ __forceinline__ void dp_operands(const float* __restrict__ dh, long grow, int c16, int q4, float4 (&df)[2],
+                                            float (&dt)[2]) {
+    const float* dhr = dh + grow * kRowF;
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const float x0 = v[2 * k], x1 = v[2 * k + 1];
-        h[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){x0, x1}, bf2));
-        const float r0 = x0 - __uint_as_float(h[k] << 16), r1 = x1 - __uint_as_float(h[k] & 0xFFFF0000u);
-        m[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){r0, r1}, bf2));
-        const float s0 = r0 - __uint_as_float(m[k] << 16), s1 = r1 - __uint_as_float(m[k] & 0xFFFF0000u);
-        l[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){s0, s1}, bf2));
+    for (int t = 0; t < 2; t++) {
+        const int r = 16 * t + c16, rc = min(r, kTok - 1);
+        df[t] = *reinterpret_cast<const float4*>(dhr + rc * kEmb + 4 * q4);
+        dt[t] = dhr[rc * kEmb + 16 + q4];
+        if (r >= kTok) df[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r >= kTok) dt[t] = 0.f;
     }
-    p[0] = __builtin_bit_cast(s16x4, make_uint2(h[0], h[1]));
-    p[1] = __builtin_bit_cast(s16x4, make_uint2(m[0], m[1]));
-    p[2] = __builtin_bit_cast(s16x4, make_uint2(l[0], l[1]));
 }
 
-// acc += A B over one k-block of 16 (fp32-class: the six partial products >= 2^-16 |ab|, small terms first)
-__device__ __forceinline__ f32x4_t mma16x3(const s16x4 (&a)[3], const s16x4 (&b)[3], f32x4_t acc) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[2], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[1], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a[0], b[0], acc, 0, 0, 0);
-    return acc;
-}
-
-constexpr int kMmaPitch = 32;  // dS transpose buffer row pitch (floats)
-constexpr int kMG = 0, kMD = kTok * kQkv, kMX = kMD + kTok * kEmb;  // reduction operands per sample
-constexpr int kMmaSample = kMX + kTok * kPin;                       // 1,472 floats (>= the 32 x 32 transpose)
-static_assert(kMmaSample >= 32 * kMmaPitch, "the dS transpose lives in the sample's region");
-
-__global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd_mfma(const float* __restrict__ ws,
+__global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* __restrict__ ws,
                                                                    const float* __restrict__ x, int ldx, int B,
                                                                    int parity, const float* __restrict__ dh,
                                                                    float* __restrict__ partial) {
-    // per sample: the reduction operands G [23][40] | dctx [23][20] | x [23][4] (the first 1,024 floats
-    // serve as the sample's dS transpose buffer before G is written); the folded maps A | c staged once
-    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kMmaSample];
-    __shared__ __attribute__((aligned(16))) float tA[kTok * kQkv * kPin];
-    __shared__ __attribute__((aligned(16))) float tC[kTok * kQkv];
-    {
-        constexpr int kN = kTok * kQkv * kPin + kTok * kQkv, kPer = (kN + kBwdThreads - 1) / kBwdThreads;
-        float v[kPer];
-#pragma unroll
-        for (int u = 0; u < kPer; u++) {
-            const int e = threadIdx.x + kBwdThreads * u;
-            v[u] = e < kN ? ws[e < kTok * kQkv * kPin ? kWsA + e : kWsC + e - kTok * kQkv * kPin] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < kPer; u++) {
-            const int e = threadIdx.x + kBwdThreads * u;
-            if (e < kTok * kQkv * kPin) tA[e] = v[u];
-            else if (e < kN) tC[e - kTok * kQkv * kPin] = v[u];
-        }
-    }
+    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kMSample];
     const int wave = threadIdx.x >> 6;
     EFAcc ef;
     ef_zero(ef);
-    const float* const fA = tA;  // folded maps [23][40][4] (LDS)
-    const float* const fC = tC;  // [23][40]
-    // output r (0-9 q, 10-19 k, 20-39 v) of token t for input slice xv; 0 for padding tokens
-    auto qkv = [&](int t, int r, float4 xv) -> float {
-        if (t >= kTok) return 0.f;
-        const float4 w = *reinterpret_cast<const float4*>(fA + (t * kQkv + r) * kPin);
-        float acc = w.x * xv.x;
-        acc = fmaf(w.y, xv.y, acc);
-        acc = fmaf(w.z, xv.z, acc);
-        acc = fmaf(w.w, xv.w, acc);
-        return acc + fC[t * kQkv + r];
-    };
     const int iters = (B + kBwdRows - 1) / kBwdRows;
+    const int tok = threadIdx.x & 31, hs = 2 * wave + ((threadIdx.x >> 5) & 1);
+    const int pc16 = threadIdx.x & 15, pq4 = (threadIdx.x >> 4) & 3;
+#if FRONT_MFMA_PREFETCH
+    // the next operands: this lane's x slice for phase 1 and the dP operands of the wave's next sample
+    float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ndf[2];
+    float ndt[2];
+    auto prefetch_iter = [&](int it2) {
+        const int r0 = it2 * kBwdRows, n2 = min(kBwdRows, B - r0);
+        if (it2 < iters && hs < n2 && tok < kTok) nx = xslice(x + (size_t)(r0 + hs) * ldx, tok, parity != 0);
+        if (it2 < iters && 2 * wave < n2) dp_operands(dh, r0 + 2 * wave, pc16, pq4, ndf, ndt);
+    };
+    prefetch_iter(blockIdx.x);
+#endif
     for (int it = blockIdx.x; it < iters; it += gridDim.x) {
         const int row0 = it * kBwdRows;
         const int nrow = min(kBwdRows, B - row0);
         __syncthreads();  // previous iteration's reduction readers are done
+        // ---- phase 1: lane (half h, token t) forms q|k|v of token t of sample 2 wave + h ----
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (hs < nrow) {
+            float4* q = reinterpret_cast<float4*>(sm + hs * kMSample + tok * kQp);
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (tok < kTok) {
+#if FRONT_MFMA_PREFETCH
+                xv = nx;
+#else
+                xv = xslice(x + (size_t)(row0 + hs) * ldx, tok, parity != 0);
+#endif
+                float o[kQkv];
+#ifdef FRONT_DIAG_NO_P1LOAD  // timing diagnostic (wrong results): no folded-map table loads
+#pragma unroll
+                for (int r = 0; r < kQkv; r++) o[r] = xv.x * (r + 1) + xv.y;
+#else
+                affine4t<kQkv>(ws + kWsAT + tok * kQkv * kPin, ws + kWsC + tok * kQkv, xv, o);
+#endif
+                q[0] = make_float4(o[0], o[1], o[2], o[3]);
+                q[1] = make_float4(o[4], o[5], o[6], o[7]);
+                q[2] = make_float4(o[8], o[9], 0.f, 0.f);
+                q[3] = make_float4(o[10], o[11], o[12], o[13]);
+                q[4] = make_float4(o[14], o[15], o[16], o[17]);
+                q[5] = make_float4(o[18], o[19], 0.f, 0.f);
+#pragma unroll
+                for (int c = 0; c < kEmb / 4; c++)
+                    q[6 + c] = make_float4(o[20 + 4 * c], o[21 + 4 * c], o[22 + 4 * c], o[23 + 4 * c]);
+            } else {
+#pragma unroll
+                for (int c = 0; c < kQp / 4; c++) q[c] = z;
+            }
+        }
+        wave_sync();
 #pragma unroll 1
         for (int half = 0; half < 2; half++) {
-            const int slot = 2 * wave + half;  // this wave's sample of the iteration
-            if (slot >= nrow) break;           // wave-uniform
-            // lane indices recomputed per sample behind an opaque copy: otherwise the compiler hoists every
-            // lane-dependent table address out of the loop and spills them
+            const int slot = 2 * wave + half;
+            if (slot >= nrow) break;  // wave-uniform
+            // lane indices recomputed per sample behind an opaque copy (no hoisted, spilled lane addresses)
             int lane = threadIdx.x & 63;
             asm volatile("" : "+v"(lane));
-            const int c16 = lane & 15, q4 = lane >> 4;
-            const int row = row0 + slot;
-            const float* xr = x + (size_t)row * ldx;
-            const float* dhr = dh + (size_t)row * kRowF;
-            float* my = sm + slot * kMmaSample;
-            float* const tbuf = my;  // dS transpose (dead before G is written: one wave, LDS in program order)
-            // the 23 token input slices -> the sample's X rows (also the reduction's operand), then every
-            // q/k/v value reads its slice from LDS
-            const float* const X = my + kMX;
-            if (lane < kTok) *reinterpret_cast<float4*>(my + kMX + lane * kPin) = xslice(xr, lane, parity != 0);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            auto xk = [&](int tok) {
-                return tok < kTok ? *reinterpret_cast<const float4*>(X + tok * kPin) : make_float4(0.f, 0.f, 0.f, 0.f);
-            };
-            float4 xrow[2] = {xk(c16), xk(c16 + 16)};
-            // ---- S = Q K^T (d_k 10 -> one k-block of 16) ----
-            s16x4 aq[2][3], bk[2][3];
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-                float v[4], w[4];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int k = 4 * q4 + e;
-                    v[e] = k < kKq ? qkv(c16 + 16 * t, k, xrow[t]) : 0.f;
-                    w[e] = k < kKq ? qkv(c16 + 16 * t, kKq + k, xrow[t]) : 0.f;
-                }
-                split4(v, aq[t]);
-                split4(w, bk[t]);
-            }
-            f32x4_t P[2][2];
-#pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++) P[ti][tj] = mma16x3(aq[ti], bk[tj], f32x4_t{0.f, 0.f, 0.f, 0.f});
-            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
-            // ---- dP = dctx V^T (d_v 20 -> two k-blocks); dS later overwrites it in place ----
-            f32x4_t dP[2][2];
-#pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++) dP[ti][tj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int kb = 0; kb < 2; kb++) {
-                const int d0 = 16 * kb + 4 * q4;  // this lane's 4 d's
-                s16x4 ad[2][3], bv[2][3];
+            const int c16 = lane & 15, q4 = (lane >> 4) & 3;
+            const float* dhr = dh + (size_t)(row0 + slot) * kRowF;
+            float* my = sm + slot * kMSample;
+            const float* QKV = my;
+            float4 df[2];
+            float dt[2];
+#if FRONT_MFMA_PREFETCH
+            df[0] = ndf[0], df[1] = ndf[1], dt[0] = ndt[0], dt[1] = ndt[1];
+            if (half == 0 && slot + 1 < nrow) dp_operands(dh, row0 + slot + 1, pc16, pq4, ndf, ndt);
+#elif defined(FRONT_DIAG_NO_DH)  // timing diagnostic (wrong results): no dh loads for dP
+            df[0] = df[1] = make_float4(1.f, 2.f, 3.f, 4.f), dt[0] = dt[1] = 1.f;
+#else
+            dp_operands(dh, row0 + slot, c16, q4, df, dt);
+#endif
+            // ---- S^T = K Q^T: tiles [J][I]; k = a = 4 q4 + e (d_k 10: q4 = 3 holds no a) ----
+            f32x4_t S[2][2];
+            {
+                const int qa = min(q4, 2);
+                float4 kf[2], qf[2];
 #pragma unroll
                 for (int t = 0; t < 2; t++) {
-                    const int tok = c16 + 16 * t;
-                    float v[4] = {0.f, 0.f, 0.f, 0.f}, w[4];
-                    if (tok < kTok && d0 < kEmb) {
-                        const float4 d4 = *reinterpret_cast<const float4*>(dhr + tok * kEmb + d0);
-                        v[0] = d4.x; v[1] = d4.y; v[2] = d4.z; v[3] = d4.w;
-                    }
-#pragma unroll
-                    for (int e = 0; e < 4; e++) w[e] = d0 + e < kEmb ? qkv(tok, 2 * kKq + d0 + e, xrow[t]) : 0.f;
-                    split4(v, ad[t]);
-                    split4(w, bv[t]);
+                    kf[t] = *reinterpret_cast<const float4*>(QKV + (16 * t + c16) * kQp + kKO + 4 * qa);
+                    qf[t] = *reinterpret_cast<const float4*>(QKV + (16 * t + c16) * kQp + kQO + 4 * qa);
+                    if (q4 == 3) kf[t] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
 #pragma unroll
-                for (int ti = 0; ti < 2; ti++)
+                for (int J = 0; J < 2; J++)
 #pragma unroll
-                    for (int tj = 0; tj < 2; tj++) dP[ti][tj] = mma16x3(ad[ti], bv[tj], dP[ti][tj]);
+                    for (int I = 0; I < 2; I++) {
+                        f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int e = 0; e < 4; e++) acc = mfma4(f4at(kf[J], e), f4at(qf[I], e), acc);
+                        S[J][I] = acc;
+                    }
             }
-            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
-            // ---- softmax rows (the reference's order: / sqrt(10), exp(x - max), * (1 / sum)) and dS ----
-#pragma unroll
-            for (int ti = 0; ti < 2; ti++) {
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const bool rowok = 16 * ti + 4 * q4 + g < kTok;
-                    float s[2];
-                    float mx = -INFINITY;
-#pragma unroll
-                    for (int tj = 0; tj < 2; tj++) {
-                        s[tj] = (16 * tj + c16 < kTok) ? div_sqrt_kq(P[ti][tj][g]) : -INFINITY;
-                        mx = fmaxf(mx, s[tj]);
-                    }
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
-                    float sum = 0.f;
-#pragma unroll
-                    for (int tj = 0; tj < 2; tj++) {
-                        s[tj] = (16 * tj + c16 < kTok) ? expf(s[tj] - mx) : 0.f;
-                        sum += s[tj];
-                    }
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 16);
-                    const float inv = 1.f / sum;
-                    float rs = 0.f;
-#pragma unroll
-                    for (int tj = 0; tj < 2; tj++) {
-                        const float p = rowok ? s[tj] * inv : 0.f;
-                        P[ti][tj][g] = p;
-                        rs = fmaf(dP[ti][tj][g], p, rs);
-                    }
-#pragma unroll
-                    for (int o = 1; o < 16; o <<= 1) rs += __shfl_xor(rs, o, 16);
-#pragma unroll
-                    for (int tj = 0; tj < 2; tj++)
-                        dP[ti][tj][g] = div_sqrt_kq(P[ti][tj][g] * (dP[ti][tj][g] - rs));  // = dS
-                }
-            }
-            f32x4_t (&dS)[2][2] = dP;
-            __builtin_amdgcn_sched_barrier(0);
+            // ---- dP^T = V dctx^T; k = c: 4 q4 + e (c < 16, float4 operands), then 16 + q4 ----
+            f32x4_t dP[2][2];
             {
-                {
+                float4 vf[2];
+                float vt[2];
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const int r = 16 * t + c16;
+                    vf[t] = *reinterpret_cast<const float4*>(QKV + r * kQp + kVO + 4 * q4);
+                    vt[t] = QKV[r * kQp + kVO + 16 + q4];
                 }
+#pragma unroll
+                for (int J = 0; J < 2; J++)
+#pragma unroll
+                    for (int I = 0; I < 2; I++) {
+                        f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int e = 0; e < 4; e++) acc = mfma4(f4at(vf[J], e), f4at(df[I], e), acc);
+                        dP[J][I] = mfma4(vt[J], dt[I], acc);
+                    }
             }
-            // ---- dS through LDS (row-major [i][j]) for dQ's A operand ----
+            // operands of dK (B: q of rows i = 16 t + 4 q4 + e, column c16) and dQ^T (A: k of rows
+            // j = 16 t + 4 q4 + e, column c16), from the zero pads for c16 >= 10; read before the QKV words
+            // are reused
+            float qb[2][4], ka[2][4];
+            {
+                const int ca = min(c16, kKq);
 #pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++)
-#pragma unroll
-                    for (int g = 0; g < 4; g++) tbuf[(16 * ti + 4 * q4 + g) * kMmaPitch + 16 * tj + c16] = dS[ti][tj][g];
-            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
-            // ---- dV^T = dctx^T P  (rows d, columns j; k = i) ----
-            f32x4_t dVt[2][2];
-#pragma unroll
-            for (int td = 0; td < 2; td++)
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++) dVt[td][tj] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            // ---- dK^T = Q^T dS  (rows k, columns j; k-dim = i) ----
-            f32x4_t dKt[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-            for (int ib = 0; ib < 2; ib++) {
-                s16x4 bp[2][3], bs[2][3];
-#pragma unroll
-                for (int tj = 0; tj < 2; tj++) {
-                    const float pv[4] = {P[ib][tj][0], P[ib][tj][1], P[ib][tj][2], P[ib][tj][3]};
-                    const float sv[4] = {dS[ib][tj][0], dS[ib][tj][1], dS[ib][tj][2], dS[ib][tj][3]};
-                    split4(pv, bp[tj]);
-                    split4(sv, bs[tj]);
-                }
-#pragma unroll
-                for (int td = 0; td < 2; td++) {
-                    const int d = 16 * td + c16;
-                    float v[4];
+                for (int t = 0; t < 2; t++)
 #pragma unroll
                     for (int e = 0; e < 4; e++) {
-                        const int i = 16 * ib + 4 * q4 + e;
-                        v[e] = (i < kTok && d < kEmb) ? dhr[i * kEmb + d] : 0.f;
+                        const int r = 16 * t + 4 * q4 + e;
+                        qb[t][e] = QKV[r * kQp + kQO + ca];
+                        ka[t][e] = QKV[r * kQp + kKO + ca];
                     }
-                    s16x4 a[3];
-                    split4(v, a);
-#pragma unroll
-                    for (int tj = 0; tj < 2; tj++) dVt[td][tj] = mma16x3(a, bp[tj], dVt[td][tj]);
-                }
-                {
-                    float v[4];
-#pragma unroll
-                    for (int e = 0; e < 4; e++)
-                        v[e] = c16 < kKq ? qkv(16 * ib + 4 * q4 + e, c16, xk(16 * ib + 4 * q4 + e)) : 0.f;
-                    s16x4 a[3];
-                    split4(v, a);
-#pragma unroll
-                    for (int tj = 0; tj < 2; tj++) dKt[tj] = mma16x3(a, bs[tj], dKt[tj]);
-                }
             }
-            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
-            // ---- dQ = dS K  (rows i, columns k; k-dim = j) ----
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            f32x4_t dQ[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+            // ---- softmax over j per query column i, then dS^T = P (dP - rowsum(P dP)) / sqrt(10) in place
+            // of dP^T; padding rows j (k = 0, so S = 0) are kept out of the max and the sum ----
 #pragma unroll
-            for (int jb = 0; jb < 2; jb++) {
-                float w[4];
+            for (int I = 0; I < 2; I++) {
+                float mx = -INFINITY;
 #pragma unroll
-                for (int e = 0; e < 4; e++)
-                    w[e] = c16 < kKq ? qkv(16 * jb + 4 * q4 + e, kKq + c16, xk(16 * jb + 4 * q4 + e)) : 0.f;
-                s16x4 b[3];
-                split4(w, b);
+                for (int J = 0; J < 2; J++)
 #pragma unroll
-                for (int ti = 0; ti < 2; ti++) {
-                    const float4 r4 = *reinterpret_cast<const float4*>(tbuf + (16 * ti + c16) * kMmaPitch + 16 * jb +
-                                                                       4 * q4);
-                    const float v[4] = {r4.x, r4.y, r4.z, r4.w};
-                    s16x4 a[3];
-                    split4(v, a);
-                    dQ[ti] = mma16x3(a, b, dQ[ti]);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);  // (register pressure: no hoisting across sections)
-            // ---- the reduction operands of this sample: G = [dq | dk | dv], dctx, x ----
+                    for (int g = 0; g < 4; g++)
+                        if (16 * J + 4 * q4 + g < kTok) mx = fmaxf(mx, S[J][I][g]);
+                mx = xq_max(mx);
+                float sum = 0.f;
 #pragma unroll
-            for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int i = 16 * ti + 4 * q4 + g;
-                    if (i < kTok && c16 < kKq) my[kMG + i * kQkv + c16] = dQ[ti][g];
-                }
-#pragma unroll
-            for (int tj = 0; tj < 2; tj++) {
-                const int j = 16 * tj + c16;
-                if (j < kTok) {
+                for (int J = 0; J < 2; J++)
 #pragma unroll
                     for (int g = 0; g < 4; g++) {
-                        const int k = 4 * q4 + g;
-                        if (k < kKq) my[kMG + j * kQkv + kKq + k] = dKt[tj][g];
+                        float e = __builtin_amdgcn_exp2f((S[J][I][g] - mx) * kLog2eRsqrtKq);
+                        e = 16 * J + 4 * q4 + g < kTok ? e : 0.f;
+                        S[J][I][g] = e;
+                        sum += e;
                     }
+                // P = 0 in the padding columns i (their dctx rows are not read as zeros below)
+                const float inv = 16 * I + c16 < kTok ? __builtin_amdgcn_rcpf(xq_sum(sum)) : 0.f;
+                float rs = 0.f;
 #pragma unroll
-                    for (int td = 0; td < 2; td++) {
-                        const int d0 = 16 * td + 4 * q4;
-                        if (d0 < kEmb)
-                            *reinterpret_cast<float4*>(my + kMG + j * kQkv + 2 * kKq + d0) =
-                                make_float4(dVt[td][tj][0], dVt[td][tj][1], dVt[td][tj][2], dVt[td][tj][3]);
+                for (int J = 0; J < 2; J++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) {
+                        const float p = S[J][I][g] * inv;
+                        S[J][I][g] = p;
+                        rs = fmaf(dP[J][I][g], p, rs);
                     }
-                }
+                rs = xq_sum(rs);
+#pragma unroll
+                for (int J = 0; J < 2; J++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++) dP[J][I][g] = (S[J][I][g] * (dP[J][I][g] - rs)) * kRSqrtKq;
             }
+            f32x4_t (&P)[2][2] = S;
+            f32x4_t (&dS)[2][2] = dP;
+            // ---- dQ^T = K^T dS^T: rows a = 4 q4 + g (10 of 16), columns i; B = the dS^T tiles ----
+            f32x4_t dQ[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int J = 0; J < 2; J++)
+#pragma unroll
+                for (int g = 0; g < 4; g++)
+#pragma unroll
+                    for (int I = 0; I < 2; I++) dQ[I] = mfma4(ka[J][g], dS[J][I][g], dQ[I]);
+            wave_sync();  // the QKV words are dead: the transpose buffer (rows j < 23) and the dctx rows
+            float* T = my;
             for (int e = lane; e < kTok * kEmb / 4; e += 64)
                 *reinterpret_cast<float4*>(my + kMD + 4 * e) = *reinterpret_cast<const float4*>(dhr + 4 * e);
+            // ---- dV = P^T dctx: rows j, columns c (20 -> 32); k = i = 16 ib + 4 q4 + e ----
+#pragma unroll
+            for (int J = 0; J < 2; J++)
+#pragma unroll
+                for (int I = 0; I < 2; I++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++)
+                        if (16 * J + 4 * q4 + g < kTok) T[(16 * J + 4 * q4 + g) * kTp + 16 * I + c16] = P[J][I][g];
+            wave_sync();
+            f32x4_t dV[2][2];
+#pragma unroll
+            for (int J = 0; J < 2; J++)
+#pragma unroll
+                for (int C = 0; C < 2; C++) dV[J][C] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ib = 0; ib < 2; ib++) {
+                float4 pa[2];
+#pragma unroll
+                for (int J = 0; J < 2; J++)
+                    pa[J] = *reinterpret_cast<const float4*>(T + (16 * J + c16) * kTp + 16 * ib + 4 * q4);
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    // dctx rows from LDS (P^T is 0 in the columns i >= 23, whose clamped rows are finite;
+                    // columns c >= 20 read the next row: those dV columns are not kept)
+                    const float* dr = my + kMD + min(16 * ib + 4 * q4 + e, kTok - 1) * kEmb + c16;
+                    const float db[2] = {dr[0], dr[16]};
+#pragma unroll
+                    for (int J = 0; J < 2; J++)
+#pragma unroll
+                        for (int C = 0; C < 2; C++) dV[J][C] = mfma4(f4at(pa[J], e), db[C], dV[J][C]);
+                }
+            }
+            wave_sync();  // P^T reads done: dS^T into the same buffer
+#pragma unroll
+            for (int J = 0; J < 2; J++)
+#pragma unroll
+                for (int I = 0; I < 2; I++)
+#pragma unroll
+                    for (int g = 0; g < 4; g++)
+                        if (16 * J + 4 * q4 + g < kTok) T[(16 * J + 4 * q4 + g) * kTp + 16 * I + c16] = dS[J][I][g];
+            wave_sync();
+            // ---- dK = dS^T Q: rows j, columns a (10 of 16); k = i = 16 ib + 4 q4 + e ----
+            f32x4_t dK[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+            for (int ib = 0; ib < 2; ib++) {
+                float4 sa[2];
+#pragma unroll
+                for (int J = 0; J < 2; J++)
+                    sa[J] = *reinterpret_cast<const float4*>(T + (16 * J + c16) * kTp + 16 * ib + 4 * q4);
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+#pragma unroll
+                    for (int J = 0; J < 2; J++) dK[J] = mfma4(f4at(sa[J], e), qb[ib][e], dK[J]);
+            }
+            wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
+#pragma unroll
+            for (int I = 0; I < 2; I++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int i = 16 * I + c16, a = 4 * q4 + g;
+                    if (i < kTok && a < kKq) my[kMG + i * kQkv + a] = dQ[I][g];
+                }
+#pragma unroll
+            for (int J = 0; J < 2; J++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int j = 16 * J + 4 * q4 + g;
+                    if (j < kTok) {
+                        if (c16 < kKq) my[kMG + j * kQkv + kKq + c16] = dK[J][g];
+#pragma unroll
+                        for (int C = 0; C < 2; C++)
+                            if (16 * C + c16 < kEmb) my[kMG + j * kQkv + 2 * kKq + 16 * C + c16] = dV[J][C][g];
+                    }
+                }
         }
+        // the X rows (the reduction's x operand; phase 1's lanes hold them), now that both samples' QKV words are dead
+        if (hs < nrow && tok < kTok) *reinterpret_cast<float4*>(sm + hs * kMSample + kMX + tok * kPin) = xv;
+#if FRONT_MFMA_PREFETCH
+        prefetch_iter(it + gridDim.x);  // in flight during the E/F phase
+#endif
         __syncthreads();
-        ef_accumulate<kMmaSample, kMG, kMD, kMX>(sm, nrow, ef);
+#ifndef FRONT_DIAG_NO_EF  // timing diagnostic (wrong results): no E/F accumulation
+        ef_accumulate<kMSample, kMG, kMD, kMX>(sm, nrow, ef);
+#endif
     }
     ef_write(partial, ef);
 }

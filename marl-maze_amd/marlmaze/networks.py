@@ -81,9 +81,16 @@ class m_Attention(nn.Module):
 
 
 _CUS = {}
-# the front-end backward's attention products: "valu" (fp32 FMA, the default) or "mfma" (bf16x3 MFMA tiles;
-# measured slower, csrc/actor_front.hip k_front_bwd_mfma)
+# the front-end backward's attention products: "valu" (fp32 FMA, one lane per token) or "mfma" (fp32 MFMA
+# tiles, csrc/actor_front.hip k_front_bwd_mfma)
 FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "valu")
+
+
+def _front_bwd_grid(B, dev):
+    """Persistent grid of the front-end backward: 8-sample workgroups, two per CU (VALU kernel, 63 KB of
+    LDS) or three (MFMA kernel, 47 KB)."""
+    per_cu = 3 if FRONT_BWD_ALGO == "mfma" else 2
+    return max(1, min(per_cu * _cu_count(dev), (B + 7) // 8))
 # the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads) or "row1" (one per lane);
 # bit-identical outputs (csrc/actor_front.hip k_front_fwd2 / k_front_fwd)
 FRONT_FWD_ALGO = _os.environ.get("MARLMAZE_FRONT_FWD", "row1")
@@ -121,7 +128,7 @@ class _FusedFront(torch.autograd.Function):
         B = x.shape[0]
         dh = dh.contiguous()
         L = _lib.lib()
-        grid = max(1, min(2 * _cu_count(x.device), (B + 7) // 8))  # two 8-sample workgroups per CU
+        grid = _front_bwd_grid(B, x.device)
         plen = L.mm_actor_front_partial_len()
         partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
         red = torch.empty(plen, dtype=torch.float32, device=x.device)
@@ -526,7 +533,7 @@ def _front_bwd_to(ws, x, parity, dh, grads):
     L = _lib.lib()
     B = x.shape[0]
     dh = dh.contiguous()
-    grid = max(1, min(2 * _cu_count(x.device), (B + 7) // 8))  # two 8-sample workgroups per CU
+    grid = _front_bwd_grid(B, x.device)
     plen = L.mm_actor_front_partial_len()
     partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
     red = torch.empty(plen, dtype=torch.float32, device=x.device)

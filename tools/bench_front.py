@@ -10,6 +10,7 @@ import torch  # noqa: E402
 from marlmaze.networks import Actor, _FusedFront, front_params  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 419430
+PARITY = (sys.argv[2] != "0") if len(sys.argv) > 2 else True
 torch.manual_seed(0)
 actor = Actor([264, 264, 264]).cuda()
 pr, at = actor.projection, actor.attention
@@ -19,7 +20,7 @@ params = front_params(pr, at)
 
 
 def fwd():
-    return _FusedFront.apply(x, True, *params)
+    return _FusedFront.apply(x, PARITY, *params)
 
 
 def step():
@@ -41,4 +42,6 @@ for name, fn in (("fwd", fwd), ("fwd+bwd", step)):
     res[name + "_ms"] = e0.elapsed_time(e1) / 10
 res["bwd_ms"] = res["fwd+bwd_ms"] - res["fwd_ms"]
 res["rows"] = B
+res["parity"] = PARITY
+res["bwd_algo"] = os.environ.get("MARLMAZE_FRONT_BWD", "valu")
 print(json.dumps(res))
