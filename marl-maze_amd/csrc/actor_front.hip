@@ -762,8 +762,9 @@ __global__ __launch_bounds__(kBwdThreads, 2) void k_front_bwd(const float* __res
 // float4 (one per 4 MFMAs) or from a zero pad (no exec-masked loads); the
 // region is reused for the transposes once the operands are in registers, then
 // for the reduction operands G = [dq | dk | dv], dctx and x of k_front_bwd,
-// whose E/F accumulation phase follows unchanged.  5.9 KB of LDS per sample,
-// 47 KB per 8-sample workgroup: three workgroups per CU.  The softmax runs on
+// whose E/F accumulation phase follows (dctx read from dh).  4 KB of LDS per
+// sample plus the folded maps staged once (18.8 KB): 51 KB per 8-sample
+// workgroup, three workgroups per CU.  The softmax runs on
 // exp2 / rcp (v_exp_f32, v_rcp_f32: ~1 ulp; the reference's
 // exp(x / sqrt(10) - max) * (1 / sum) within ~3e-7 relative).
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
@@ -771,12 +772,16 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 constexpr int kQp = 44;                      // QKV row pitch (floats): [32 tokens][44]
 constexpr int kQO = 0, kKO = 12, kVO = 24;   // q | 0 0 | k | 0 0 | v
 constexpr int kTp = 36;                      // transpose buffer T [j][i], pitch 36 (j-major)
-// reduction operands G [23][40] | dctx [23][20] | x [23][4]: 0, 936, 1396 (dctx 16 words past G's end: the E/F
-// phase's 16-byte reads of a token's G and dctx rows fall in different LDS banks)
-constexpr int kMG = 0, kMD = kTok * kQkv + 16, kMX = kMD + kTok * kEmb;
-constexpr int kMSample = kMX + kTok * kPin;  // 1,488 floats per sample
-static_assert(32 * kQp <= kMSample && 32 * kTp <= kMSample, "QKV and T live in the sample's region");
-static_assert(kTok * kTp <= kMD, "the transpose rows j < 23 stay below dctx");
+// per sample: QKV [23][44], then T [23][36], then the reduction operands G [23][40] | x [23][4] (dctx is
+// read from dh).  The padding tokens' rows 23-31 of QKV and T are read past the rows written -- the next
+// words of the workgroup's LDS, zeroed at the start, finite ever after: every product keeps them out of
+// the results (S^T and dP^T rows / columns >= 23 are masked out of the softmax, P and dS are 0 there)
+constexpr int kMG = 0, kMX = kTok * kQkv;
+constexpr int kMSample = kMX + kTok * kPin;  // 1,012 floats per sample
+static_assert(kTok * kQp <= kMSample && kTok * kTp <= kMSample, "QKV and T live in the sample's region");
+// zeroed words after the last sample's region, so that its padding rows read this kernel's own data (words
+// of another kernel could hold anything, and a huge finite value times the zero weight it gets is not 0)
+constexpr int kMPad = ((32 * kQp > 32 * kTp ? 32 * kQp : 32 * kTp) - kMSample + 3) & ~3;
 constexpr float kLog2eRsqrtKq = 1.44269504088896341f * 0.316227766016838f;  // log2(e) / sqrt(10)
 
 __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
@@ -804,7 +809,7 @@ __device__ __forceinline__ float xq_max(float v) {
 }
 
 #ifndef FRONT_MFMA_PREFETCH
-#define FRONT_MFMA_PREFETCH 0  // 1: global operands loaded one sample / iteration ahead (16 spilled VGPRs: slower)
+#define FRONT_MFMA_PREFETCH 0  // 1: global operands loaded one sample / iteration ahead (measured slower)
 #endif
 
 // dP^T's B operand of one sample (dh row grow): rows 16 t + c16 (zero past token 22), columns 4 q4 .. 4 q4 + 3
@@ -822,12 +827,99 @@ __device__ __forceinline__ void dp_operands(const float* __restrict__ dh, long g
     }
 }
 
+constexpr int kTabS = kQkv * kPin + kQkv + 4;  // staged folded map per token: A^T [4][40] | c [40] | pad; 204 words:
+                                               // 16 lanes' 16-byte reads of 16 tokens hit disjoint banks
+
+// E/F phase of k_front_bwd_mfma, with the dctx rows read from dh (L2-resident: the samples' dP operands were
+// just read from them) instead of LDS.  Units 0-229: G rows (token u / 10, rows 4 (u % 10)); 230-344: dctx
+// rows (token (u - 230) / 5, rows 40 + 4 ((u - 230) % 5)).  Thread t owns units t and t + 256, so at most one
+// dctx unit, whose rows for all the iteration's samples are loaded up front (ef2_prefetch, before the barrier)
+static_assert(kEFR == 4, "k_front_bwd_mfma's E/F units are 4 rows");
+constexpr int kEF2G = kTok * kQkv / 4;  // 230 G units
+
+__device__ __forceinline__ void ef2_unit(int unit, int& tk, int& r0) {
+    if (unit < kEF2G) {
+        tk = unit / (kQkv / 4);
+        r0 = 4 * (unit % (kQkv / 4));
+    } else {
+        tk = (unit - kEF2G) / (kEmb / 4);
+        r0 = kQkv + 4 * ((unit - kEF2G) % (kEmb / 4));
+    }
+}
+
+__device__ __forceinline__ void ef2_prefetch(const float* __restrict__ dh0, int nrow, float4 (&fp)[kBwdRows]) {
+    const int fu = threadIdx.x < kEF2G ? threadIdx.x + kBwdThreads : threadIdx.x;
+    int tk, r0;
+    ef2_unit(fu, tk, r0);
+    const bool has = fu < kEFUnits;
+#pragma unroll
+    for (int gg = 0; gg < kBwdRows; gg++)
+        fp[gg] = (has && gg < nrow) ? *reinterpret_cast<const float4*>(dh0 + (size_t)gg * kRowF + tk * kEmb + r0 - kQkv)
+                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+template <int kStride, int kG, int kX>
+__device__ __forceinline__ void ef2_accumulate(const float* sm, int nrow, const float4 (&fp)[kBwdRows], EFAcc& acc) {
+#pragma unroll
+    for (int u = 0; u < kEFU; u++) {
+        const int unit = threadIdx.x + u * kBwdThreads;
+        if (unit < kEFUnits) {
+            int tk, r0;
+            ef2_unit(unit, tk, r0);
+            const bool lds = unit < kEF2G;
+#pragma unroll
+            for (int gg = 0; gg < kBwdRows; gg++) {
+                if (gg < nrow) {
+                    const float* sg = sm + gg * kStride;
+                    const float4 gv = lds ? *reinterpret_cast<const float4*>(sg + kG + tk * kQkv + r0) : fp[gg];
+                    const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
+                    const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
+                    const f32x2 x01 = {xq.x, xq.y}, x23 = {xq.z, xq.w};
+#pragma unroll
+                    for (int a = 0; a < 4; a++) {
+                        const f32x2 ga = {gr[a], gr[a]};
+                        acc.e[u][a][0] = __builtin_elementwise_fma(ga, x01, acc.e[u][a][0]);
+                        acc.e[u][a][1] = __builtin_elementwise_fma(ga, x23, acc.e[u][a][1]);
+                    }
+#pragma unroll
+                    for (int a = 0; a < 2; a++) acc.s[u][a] += f32x2{gr[2 * a], gr[2 * a + 1]};
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void ef2_write(float* partial, const EFAcc& acc) {
+    float* out = partial + (size_t)blockIdx.x * kPartLen;
+#pragma unroll
+    for (int u = 0; u < kEFU; u++) {
+        const int unit = threadIdx.x + u * kBwdThreads;
+        if (unit < kEFUnits) {
+            int tk, r0;
+            ef2_unit(unit, tk, r0);
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                *reinterpret_cast<float4*>(out + kPEF + (tk * kGd + r0 + a) * kPin) =
+                    make_float4(acc.e[u][a][0].x, acc.e[u][a][0].y, acc.e[u][a][1].x, acc.e[u][a][1].y);
+                out[kPef + tk * kGd + r0 + a] = (a & 1) ? acc.s[u][a / 2].y : acc.s[u][a / 2].x;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* __restrict__ ws,
                                                                    const float* __restrict__ x, int ldx, int B,
                                                                    int parity, const float* __restrict__ dh,
                                                                    float* __restrict__ partial) {
-    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kMSample];
+    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kMSample + kMPad];
+    __shared__ __attribute__((aligned(16))) float tab[kTok * kTabS];
     const int wave = threadIdx.x >> 6;
+    for (int e = threadIdx.x; e < kBwdRows * kMSample + kMPad; e += kBwdThreads) sm[e] = 0.f;  // (see kMSample)
+    // the folded maps once per workgroup (each lane's q|k|v reads them every iteration)
+    for (int e = threadIdx.x; e < kTok * (kQkv * kPin + kQkv); e += kBwdThreads) {
+        const int t = e / (kQkv * kPin + kQkv), f = e % (kQkv * kPin + kQkv);
+        tab[t * kTabS + f] = f < kQkv * kPin ? ws[kWsAT + t * kQkv * kPin + f] : ws[kWsC + t * kQkv + f - kQkv * kPin];
+    }
     EFAcc ef;
     ef_zero(ef);
     const int iters = (B + kBwdRows - 1) / kBwdRows;
@@ -852,7 +944,6 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
         float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (hs < nrow) {
             float4* q = reinterpret_cast<float4*>(sm + hs * kMSample + tok * kQp);
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
             if (tok < kTok) {
 #if FRONT_MFMA_PREFETCH
                 xv = nx;
@@ -864,7 +955,7 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
 #pragma unroll
                 for (int r = 0; r < kQkv; r++) o[r] = xv.x * (r + 1) + xv.y;
 #else
-                affine4t<kQkv>(ws + kWsAT + tok * kQkv * kPin, ws + kWsC + tok * kQkv, xv, o);
+                affine4t<kQkv>(tab + tok * kTabS, tab + tok * kTabS + kQkv * kPin, xv, o);
 #endif
                 q[0] = make_float4(o[0], o[1], o[2], o[3]);
                 q[1] = make_float4(o[4], o[5], o[6], o[7]);
@@ -875,9 +966,6 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
 #pragma unroll
                 for (int c = 0; c < kEmb / 4; c++)
                     q[6 + c] = make_float4(o[20 + 4 * c], o[21 + 4 * c], o[22 + 4 * c], o[23 + 4 * c]);
-            } else {
-#pragma unroll
-                for (int c = 0; c < kQp / 4; c++) q[c] = z;
             }
         }
         wave_sync();
@@ -1007,10 +1095,8 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
                 for (int g = 0; g < 4; g++)
 #pragma unroll
                     for (int I = 0; I < 2; I++) dQ[I] = mfma4(ka[J][g], dS[J][I][g], dQ[I]);
-            wave_sync();  // the QKV words are dead: the transpose buffer (rows j < 23) and the dctx rows
+            wave_sync();  // the QKV words are dead: the transpose buffer (rows j < 23)
             float* T = my;
-            for (int e = lane; e < kTok * kEmb / 4; e += 64)
-                *reinterpret_cast<float4*>(my + kMD + 4 * e) = *reinterpret_cast<const float4*>(dhr + 4 * e);
             // ---- dV = P^T dctx: rows j, columns c (20 -> 32); k = i = 16 ib + 4 q4 + e ----
 #pragma unroll
             for (int J = 0; J < 2; J++)
@@ -1033,10 +1119,10 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
                     pa[J] = *reinterpret_cast<const float4*>(T + (16 * J + c16) * kTp + 16 * ib + 4 * q4);
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
-                    // dctx rows from LDS (P^T is 0 in the columns i >= 23, whose clamped rows are finite;
-                    // columns c >= 20 read the next row: those dV columns are not kept)
-                    const float* dr = my + kMD + min(16 * ib + 4 * q4 + e, kTok - 1) * kEmb + c16;
-                    const float db[2] = {dr[0], dr[16]};
+                    // dctx rows (P^T is 0 in the columns i >= 23, whose clamped rows are finite; columns
+                    // c >= 20 repeat column 19: those dV columns are not kept)
+                    const float* dr = dhr + min(16 * ib + 4 * q4 + e, kTok - 1) * kEmb;
+                    const float db[2] = {dr[c16], dr[min(16 + c16, kEmb - 1)]};
 #pragma unroll
                     for (int J = 0; J < 2; J++)
 #pragma unroll
@@ -1086,6 +1172,8 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
                     }
                 }
         }
+        float4 fp[kBwdRows];
+        ef2_prefetch(dh + (size_t)row0 * kRowF, nrow, fp);
         // the X rows (the reduction's x operand; phase 1's lanes hold them), now that both samples' QKV words are dead
         if (hs < nrow && tok < kTok) *reinterpret_cast<float4*>(sm + hs * kMSample + kMX + tok * kPin) = xv;
 #if FRONT_MFMA_PREFETCH
@@ -1093,10 +1181,10 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
 #endif
         __syncthreads();
 #ifndef FRONT_DIAG_NO_EF  // timing diagnostic (wrong results): no E/F accumulation
-        ef_accumulate<kMSample, kMG, kMD, kMX>(sm, nrow, ef);
+        ef2_accumulate<kMSample, kMG, kMX>(sm, nrow, fp, ef);
 #endif
     }
-    ef_write(partial, ef);
+    ef2_write(partial, ef);
 }
 
 // sum of the partial rows: workgroup = 64 columns x 16 row classes (r mod 16);

@@ -81,14 +81,14 @@ class m_Attention(nn.Module):
 
 
 _CUS = {}
-# the front-end backward's attention products: "valu" (fp32 FMA, one lane per token) or "mfma" (fp32 MFMA
-# tiles, csrc/actor_front.hip k_front_bwd_mfma)
-FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "valu")
+# the front-end backward's attention products: "mfma" (fp32 MFMA tiles, csrc/actor_front.hip
+# k_front_bwd_mfma; the default) or "valu" (fp32 FMA, one lane per token, k_front_bwd)
+FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "mfma")
 
 
 def _front_bwd_grid(B, dev):
     """Persistent grid of the front-end backward: 8-sample workgroups, two per CU (VALU kernel, 63 KB of
-    LDS) or three (MFMA kernel, 47 KB)."""
+    LDS) or three (MFMA kernel, 51 KB)."""
     per_cu = 3 if FRONT_BWD_ALGO == "mfma" else 2
     return max(1, min(per_cu * _cu_count(dev), (B + 7) // 8))
 # the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads) or "row1" (one per lane);
