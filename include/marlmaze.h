@@ -435,9 +435,9 @@ int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int pari
 /* mm_actor_front_bwd with the attention backward's algorithm chosen:
  * MM_FRONT_BWD_VALU (mm_actor_front_bwd's): fp32 FMA, one lane per token;
  * MM_FRONT_BWD_MFMA: the per-sample products S = QK^T, dP = dctx V^T, dV, dK,
- * dQ as 16x16x16 bf16x3 MFMA tiles (fp32-class; measured slower: 2.70 vs
- * 1.85 ms at 419,430 rows).  Same outputs and partial layout; sums in a fixed
- * order either way. */
+ * dQ on the fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fmaf chains; the faster:
+ * 1.34 vs 1.59 ms at 419,430 rows; `grid` up to 3 per CU).  Same outputs and
+ * partial layout; sums in a fixed order either way. */
 #define MM_FRONT_BWD_MFMA 0
 #define MM_FRONT_BWD_VALU 1
 int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
