@@ -783,6 +783,9 @@ static_assert(kTok * kQp <= kMSample && kTok * kTp <= kMSample, "QKV and T live 
 // of another kernel could hold anything, and a huge finite value times the zero weight it gets is not 0)
 constexpr int kMPad = ((32 * kQp > 32 * kTp ? 32 * kQp : 32 * kTp) - kMSample + 3) & ~3;
 constexpr float kLog2eRsqrtKq = 1.44269504088896341f * 0.316227766016838f;  // log2(e) / sqrt(10)
+#ifndef FRONT_MFMA_FAST_SOFTMAX  // 1: exp2 / rcp / * (1 / sqrt(10)); 0: the reference's steps (12% slower)
+#define FRONT_MFMA_FAST_SOFTMAX 1
+#endif
 
 __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -1048,28 +1051,42 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
                     }
             }
             // ---- softmax over j per query column i, then dS^T = P (dP - rowsum(P dP)) / sqrt(10) in place
-            // of dP^T; padding rows j (k = 0, so S = 0) are kept out of the max and the sum ----
+            // of dP^T; padding rows j (k = 0, so S = 0) are kept out of the max and the sum.  exp2 / rcp
+            // (~1 ulp) by default; FRONT_MFMA_FAST_SOFTMAX=0 takes the reference's rounding steps (x /
+            // sqrt(10), expf, 1 / sum, as k_front_bwd) -- the gradients' distance to fp64 is the same ----
 #pragma unroll
             for (int I = 0; I < 2; I++) {
                 float mx = -INFINITY;
 #pragma unroll
                 for (int J = 0; J < 2; J++)
 #pragma unroll
-                    for (int g = 0; g < 4; g++)
+                    for (int g = 0; g < 4; g++) {
+#if !FRONT_MFMA_FAST_SOFTMAX
+                        S[J][I][g] = div_sqrt_kq(S[J][I][g]);
+#endif
                         if (16 * J + 4 * q4 + g < kTok) mx = fmaxf(mx, S[J][I][g]);
+                    }
                 mx = xq_max(mx);
                 float sum = 0.f;
 #pragma unroll
                 for (int J = 0; J < 2; J++)
 #pragma unroll
                     for (int g = 0; g < 4; g++) {
+#if FRONT_MFMA_FAST_SOFTMAX
                         float e = __builtin_amdgcn_exp2f((S[J][I][g] - mx) * kLog2eRsqrtKq);
+#else
+                        float e = expf(S[J][I][g] - mx);
+#endif
                         e = 16 * J + 4 * q4 + g < kTok ? e : 0.f;
                         S[J][I][g] = e;
                         sum += e;
                     }
                 // P = 0 in the padding columns i (their dctx rows are not read as zeros below)
+#if FRONT_MFMA_FAST_SOFTMAX
                 const float inv = 16 * I + c16 < kTok ? __builtin_amdgcn_rcpf(xq_sum(sum)) : 0.f;
+#else
+                const float inv = 16 * I + c16 < kTok ? 1.f / xq_sum(sum) : 0.f;
+#endif
                 float rs = 0.f;
 #pragma unroll
                 for (int J = 0; J < 2; J++)
@@ -1083,7 +1100,12 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
 #pragma unroll
                 for (int J = 0; J < 2; J++)
 #pragma unroll
-                    for (int g = 0; g < 4; g++) dP[J][I][g] = (S[J][I][g] * (dP[J][I][g] - rs)) * kRSqrtKq;
+                    for (int g = 0; g < 4; g++)
+#if FRONT_MFMA_FAST_SOFTMAX
+                        dP[J][I][g] = (S[J][I][g] * (dP[J][I][g] - rs)) * kRSqrtKq;
+#else
+                        dP[J][I][g] = div_sqrt_kq(S[J][I][g] * (dP[J][I][g] - rs));
+#endif
             }
             f32x4_t (&P)[2][2] = S;
             f32x4_t (&dS)[2][2] = dP;
