@@ -1175,12 +1175,13 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
             }
             wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
 #pragma unroll
-            for (int I = 0; I < 2; I++)
-#pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int i = 16 * I + c16, a = 4 * q4 + g;
-                    if (i < kTok && a < kKq) my[kMG + i * kQkv + a] = dQ[I][g];
-                }
+            for (int I = 0; I < 2; I++) {  // dq rows a = 4 q4 .. 4 q4 + 3 of token i: one 16-byte write (a = 10, 11
+                                            // are 0 -- k's zero pad -- and rewritten with dk below)
+                const int i = 16 * I + c16;
+                if (i < kTok && q4 < 3)
+                    *reinterpret_cast<float4*>(my + kMG + i * kQkv + 4 * q4) =
+                        make_float4(dQ[I][0], dQ[I][1], dQ[I][2], dQ[I][3]);
+            }
 #pragma unroll
             for (int J = 0; J < 2; J++)
 #pragma unroll

@@ -18,7 +18,9 @@ before generation and handed back afterwards, so a program that seeds
 
 Observation values are the float32 values the reference's lists become inside
 ``PPO`` (PPO.py:144, ``torch.tensor(obs, dtype=torch.float)``).  The
-reference's pygame viewer (maze.py:276-522) is out of scope.
+reference's pygame viewer (maze.py:276-522) is drawn headless by
+``marlmaze.viewer`` (``draw_maze`` / ``display_policy`` return PIL images and
+write an animated GIF instead of opening a window).
 """
 import random
 
@@ -130,3 +132,21 @@ class Maze:
         if tuple(start) != self.start or tuple(end) != self.end:
             raise NotImplementedError("only the start -> end path of the current maze is kept on the device")
         return list(self.shortest_path)
+
+    # ---- the viewer (maze.py:276-522), headless: marlmaze.viewer ----
+    def draw_maze(self, id=-1):
+        """maze.py:277-361: the full maze (id -1) or agent `id`'s fogged view, as a PIL image."""
+        from . import viewer
+
+        return viewer.draw_maze(self, id)
+
+    def print_maze(self):  # maze.py:456-458
+        for row in self.layout:
+            print(row)
+
+    def display_policy(self, id=-1, steps=200, path=None):
+        """maze.py:466-522 without the window: `steps` policy steps from a reset, one frame per state
+        (returned; an animated GIF at `path` when given)."""
+        from . import viewer
+
+        return viewer.display_policy(self, id=id, steps=steps, path=path)

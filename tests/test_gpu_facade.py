@@ -128,3 +128,48 @@ def test_integration_snippet_runs():
     o1, m1, r1, _ = env.step(act, auto_reset=True)
     assert torch.equal(o1, ns["obs"]) and torch.equal(m1.to(torch.uint8), ns["masks"])
     assert torch.equal(r1, ns["reward"])
+
+
+def test_display_policy_headless(tmp_path):
+    """main.py:17-23 end to end, headless: PPO brain, two Agents with main.py's colours, the Maze, then
+    display_policy -- a reset and policy steps through the HIP env, one frame per state, written as a
+    GIF; every frame shows the current layout (walls black, marks in the agents' mark colours) and
+    the fogged agent view shows the agent's own cell."""
+    from PIL import Image
+
+    from marlmaze import viewer
+    from marlmaze.PPO import PPO
+
+    brain = PPO(agent_amount=2, batch_size=2000, lr=0.00014, n_envs=16, load=False, verbose=False, save=False,
+                sample_seed=6)
+    agents = (Agent("RED", brain, "red", "palevioletred1", 2), Agent("BLUE", brain, "royalblue1", "darkslategray1", 3))
+    maze = Maze(agents=agents, max_timestep=1200, rand_sizes=True, rand_range=[12, 13], rand_start=True,
+                difficulty=1, default_size=[4, 4])
+    random.seed(5)
+    path = tmp_path / "policy.gif"
+    frames = maze.display_policy(steps=6, path=str(path))
+    assert len(frames) >= 7 and path.exists()
+    assert Image.open(path).n_frames == len(frames)
+    img = np.asarray(frames[-1])
+    C = viewer.CELL_SIZE
+    assert img.shape == (maze.height * C, maze.width * C, 3)
+    lay = np.asarray(maze.layout)
+    occupied = set(maze.agent_positions) | {maze.start, maze.end} | set(map(tuple, maze.shortest_path or []))
+    if maze.key != 0:
+        occupied.add(maze.key)
+    mark_rgb = {2: viewer.rgb("palevioletred1"), 3: viewer.rgb("darkslategray1")}
+    for y in range(maze.height):
+        for x in range(maze.width):
+            px = tuple(img[y * C + 2, x * C + 2])  # a cell corner: no agent / flag / key / dot drawn there
+            if lay[y, x] == 1:
+                assert px == viewer.WALL_COLOR, (x, y)
+            elif lay[y, x] in mark_rgb and (x, y) not in occupied:
+                assert px == mark_rgb[lay[y, x]], (x, y)
+    ax, ay = agents[0].x, agents[0].y
+    fog = np.asarray(maze.draw_maze(id=2))
+    assert tuple(fog[ay * C + C // 2, ax * C + C // 2]) == viewer.rgb("red")  # the agent's body
+    assert tuple(fog[ay * C + 1, ax * C + 1]) == viewer.PATH_COLOR  # its own cell is drawn
+    far = [(x, y) for y in range(maze.height) for x in range(maze.width) if abs(x - ax) + abs(y - ay) > 12]
+    if far:
+        x, y = far[0]
+        assert tuple(fog[y * C + 2, x * C + 2]) == viewer.FOG_COLOR  # beyond any ray: fog
