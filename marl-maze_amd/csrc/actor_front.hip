@@ -791,6 +791,11 @@ __device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// the k = i steps of dV and dK: i = 4 q4 + s over the first 16 tokens (s < 4), then 16 + q4 + 4 (s - 4):
+// two steps cover tokens 16-23 (token 23 is padding: P^T and dS^T are 0 there)
+constexpr int kKH = 6;
+__device__ __forceinline__ int kh_row(int s, int q4) { return s < 4 ? 4 * q4 + s : 16 + q4 + 4 * (s - 4); }
+
 __device__ __forceinline__ float f4at(const float4& v, int e) {
     return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
 }
@@ -993,24 +998,25 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
 #else
             dp_operands(dh, row0 + slot, c16, q4, df, dt);
 #endif
-            // ---- S^T = K Q^T: tiles [J][I]; k = a = 4 q4 + e (d_k 10: q4 = 3 holds no a) ----
+            // ---- S^T = K Q^T: tiles [J][I]; k = a = q4 + 4 e, three steps over a < 12 (d_k 10: a = 10, 11
+            // read the zero pads) ----
             f32x4_t S[2][2];
             {
-                const int qa = min(q4, 2);
-                float4 kf[2], qf[2];
+                float kf[2][3], qf[2][3];
 #pragma unroll
-                for (int t = 0; t < 2; t++) {
-                    kf[t] = *reinterpret_cast<const float4*>(QKV + (16 * t + c16) * kQp + kKO + 4 * qa);
-                    qf[t] = *reinterpret_cast<const float4*>(QKV + (16 * t + c16) * kQp + kQO + 4 * qa);
-                    if (q4 == 3) kf[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-                }
+                for (int t = 0; t < 2; t++)
+#pragma unroll
+                    for (int e = 0; e < 3; e++) {
+                        kf[t][e] = QKV[(16 * t + c16) * kQp + kKO + q4 + 4 * e];
+                        qf[t][e] = QKV[(16 * t + c16) * kQp + kQO + q4 + 4 * e];
+                    }
 #pragma unroll
                 for (int J = 0; J < 2; J++)
 #pragma unroll
                     for (int I = 0; I < 2; I++) {
                         f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                        for (int e = 0; e < 4; e++) acc = mfma4(f4at(kf[J], e), f4at(qf[I], e), acc);
+                        for (int e = 0; e < 3; e++) acc = mfma4(kf[J][e], qf[I][e], acc);
                         S[J][I] = acc;
                     }
             }
@@ -1038,17 +1044,16 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
             // operands of dK (B: q of rows i = 16 t + 4 q4 + e, column c16) and dQ^T (A: k of rows
             // j = 16 t + 4 q4 + e, column c16), from the zero pads for c16 >= 10; read before the QKV words
             // are reused
-            float qb[2][4], ka[2][4];
+            // (dK's k = i runs over 16 + q4 + 4 e for the second half: two steps cover i < 24)
+            float qb[kKH], ka[2][4];
             {
                 const int ca = min(c16, kKq);
 #pragma unroll
                 for (int t = 0; t < 2; t++)
 #pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        const int r = 16 * t + 4 * q4 + e;
-                        qb[t][e] = QKV[r * kQp + kQO + ca];
-                        ka[t][e] = QKV[r * kQp + kKO + ca];
-                    }
+                    for (int e = 0; e < 4; e++) ka[t][e] = QKV[(16 * t + 4 * q4 + e) * kQp + kKO + ca];
+#pragma unroll
+                for (int s = 0; s < kKH; s++) qb[s] = QKV[kh_row(s, q4) * kQp + kQO + ca];
             }
             // ---- softmax over j per query column i, then dS^T = P (dP - rowsum(P dP)) / sqrt(10) in place
             // of dP^T; padding rows j (k = 0, so S = 0) are kept out of the max and the sum.  exp2 / rcp
@@ -1134,22 +1139,19 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
 #pragma unroll
                 for (int C = 0; C < 2; C++) dV[J][C] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int ib = 0; ib < 2; ib++) {
-                float4 pa[2];
+            for (int s = 0; s < kKH; s++) {
+                // k = i = kh_row(s, q4): P^T rows j, column i; dctx rows i (P^T is 0 in the columns i >= 23, whose
+                // clamped rows are finite; columns c >= 20 repeat column 19: those dV columns are not kept)
+                const int i = kh_row(s, q4);
+                float pa[2];
+#pragma unroll
+                for (int J = 0; J < 2; J++) pa[J] = T[(16 * J + c16) * kTp + i];
+                const float* dr = dhr + min(i, kTok - 1) * kEmb;
+                const float db[2] = {dr[c16], dr[min(16 + c16, kEmb - 1)]};
 #pragma unroll
                 for (int J = 0; J < 2; J++)
-                    pa[J] = *reinterpret_cast<const float4*>(T + (16 * J + c16) * kTp + 16 * ib + 4 * q4);
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    // dctx rows (P^T is 0 in the columns i >= 23, whose clamped rows are finite; columns
-                    // c >= 20 repeat column 19: those dV columns are not kept)
-                    const float* dr = dhr + min(16 * ib + 4 * q4 + e, kTok - 1) * kEmb;
-                    const float db[2] = {dr[c16], dr[min(16 + c16, kEmb - 1)]};
-#pragma unroll
-                    for (int J = 0; J < 2; J++)
-#pragma unroll
-                        for (int C = 0; C < 2; C++) dV[J][C] = mfma4(f4at(pa[J], e), db[C], dV[J][C]);
-                }
+                    for (int C = 0; C < 2; C++) dV[J][C] = mfma4(pa[J], db[C], dV[J][C]);
             }
             wave_sync();  // P^T reads done: dS^T into the same buffer
 #pragma unroll
@@ -1163,15 +1165,10 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
             // ---- dK = dS^T Q: rows j, columns a (10 of 16); k = i = 16 ib + 4 q4 + e ----
             f32x4_t dK[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-            for (int ib = 0; ib < 2; ib++) {
-                float4 sa[2];
+            for (int s = 0; s < kKH; s++) {
+                const int i = kh_row(s, q4);
 #pragma unroll
-                for (int J = 0; J < 2; J++)
-                    sa[J] = *reinterpret_cast<const float4*>(T + (16 * J + c16) * kTp + 16 * ib + 4 * q4);
-#pragma unroll
-                for (int e = 0; e < 4; e++)
-#pragma unroll
-                    for (int J = 0; J < 2; J++) dK[J] = mfma4(f4at(sa[J], e), qb[ib][e], dK[J]);
+                for (int J = 0; J < 2; J++) dK[J] = mfma4(T[(16 * J + c16) * kTp + i], qb[s], dK[J]);
             }
             wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
 #pragma unroll
