@@ -7,8 +7,10 @@
 // [B,23,40] split/cat copies.  Here a 32-lane group owns one sample, lane i =
 // token i (23 of 32 lanes active): its own vectors stay in registers, every
 // token's k, v (and in the backward q, P, dS) sit in LDS and are read as
-// broadcasts.  fp32 throughout (fmaf accumulation; the reference's op order
-// per element: logits / sqrt(10), softmax = exp(x - max) * (1 / sum)).
+// broadcasts.  fp32 throughout (fmaf accumulation; the softmax as exp2 of the
+// scaled logits on v_exp_f32 and v_rcp_f32 for 1 / sum by default -- ~1 ulp
+// each -- or the reference's steps, logits / sqrt(10), expf(x - max) * (1 / sum),
+// with FRONT_FWD_FAST_SOFTMAX=0 / FRONT_MFMA_FAST_SOFTMAX=0).
 //
 // Linear-map folding.  Token i's input is a <= 4-wide slice x_i, and
 //   t_i = Wp_i x_i + b_i,   [q|k|v]_i = Wqkv t_i = (Wqkv Wp_i) x_i + Wqkv b_i,
@@ -64,6 +66,38 @@ constexpr float kRSqrtKq = 0.316227766016838f;  // RN(1 / kSqrtKq)
 __device__ __forceinline__ float div_sqrt_kq(float x) {
     const float q = x * kRSqrtKq;
     return fmaf(fmaf(-q, kSqrtKq, x), kRSqrtKq, q);
+}
+
+constexpr float kLog2eRsqrtKq = 1.44269504088896341f * 0.316227766016838f;  // log2(e) / sqrt(10)
+
+// The forward's softmax steps.  FRONT_FWD_FAST_SOFTMAX=1 (default): scores kept as raw q.k, exponent
+// exp2(q.k log2(e) / sqrt(10) - max) on v_exp_f32 (one fma + one exp instead of the division and the
+// libm expf sequence), v_rcp_f32 for 1 / sum (~1 ulp each; h stays within ~3e-7 relative of the
+// reference's steps, the same form as k_front_bwd_mfma's backward).  0: the reference's steps
+// (x / sqrt(10), expf, 1 / sum).
+#ifndef FRONT_FWD_FAST_SOFTMAX
+#define FRONT_FWD_FAST_SOFTMAX 1
+#endif
+__device__ __forceinline__ float fwd_score(float qk) {
+#if FRONT_FWD_FAST_SOFTMAX
+    return qk;
+#else
+    return div_sqrt_kq(qk);
+#endif
+}
+__device__ __forceinline__ float fwd_exp(float s, float mx) {
+#if FRONT_FWD_FAST_SOFTMAX
+    return __builtin_amdgcn_exp2f(fmaf(s, kLog2eRsqrtKq, -mx * kLog2eRsqrtKq));
+#else
+    return expf(s - mx);
+#endif
+}
+__device__ __forceinline__ float fwd_rcp(float sum) {
+#if FRONT_FWD_FAST_SOFTMAX
+    return __builtin_amdgcn_rcpf(sum);
+#else
+    return 1.f / sum;
+#endif
 }
 
 // workspace (floats)
@@ -349,13 +383,13 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                s[j] = div_sqrt_kq(dot4<kKq>(q, Ks[g][j]));
+                s[j] = fwd_score(dot4<kKq>(q, Ks[g][j]));
                 mx = fmaxf(mx, s[j]);
             }
             float sum0 = 0.f, sum1 = 0.f;  // even / odd j: two short chains (the backward recomputes the same way)
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                s[j] = expf(s[j] - mx);
+                s[j] = fwd_exp(s[j], mx);
                 if (j & 1) sum1 += s[j];
                 else sum0 += s[j];
             }
@@ -363,7 +397,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
             float out[kEmb];
 #pragma unroll
             for (int c = 0; c < kEmb; c++) out[c] = 0.f;
-            const float inv = 1.f / sum;  // torch's softmax scales by the reciprocal of the sum
+            const float inv = fwd_rcp(sum);  // torch's softmax scales by the reciprocal of the sum
 #pragma unroll
             for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] * inv, Vs[g][j]);
             float t[kEmb];
@@ -449,16 +483,16 @@ __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__
             float mxa = -INFINITY, mxb = -INFINITY;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                sa[j] = div_sqrt_kq(dot4<kKq>(qa, Ks[g][j]));
-                sb[j] = div_sqrt_kq(dot4<kKq>(qb, Ks[g][j]));
+                sa[j] = fwd_score(dot4<kKq>(qa, Ks[g][j]));
+                sb[j] = fwd_score(dot4<kKq>(qb, Ks[g][j]));
                 mxa = fmaxf(mxa, sa[j]);
                 mxb = fmaxf(mxb, sb[j]);
             }
             float suma0 = 0.f, suma1 = 0.f, sumb0 = 0.f, sumb1 = 0.f;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                sa[j] = expf(sa[j] - mxa);
-                sb[j] = expf(sb[j] - mxb);
+                sa[j] = fwd_exp(sa[j], mxa);
+                sb[j] = fwd_exp(sb[j], mxb);
                 if (j & 1) {
                     suma1 += sa[j];
                     sumb1 += sb[j];
@@ -467,7 +501,7 @@ __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__
                     sumb0 += sb[j];
                 }
             }
-            const float inva = 1.f / (suma0 + suma1), invb = 1.f / (sumb0 + sumb1);
+            const float inva = fwd_rcp(suma0 + suma1), invb = fwd_rcp(sumb0 + sumb1);
             float oa[kEmb], ob[kEmb];
 #pragma unroll
             for (int c = 0; c < kEmb; c++) oa[c] = ob[c] = 0.f;
@@ -782,7 +816,6 @@ static_assert(kTok * kQp <= kMSample && kTok * kTp <= kMSample, "QKV and T live 
 // zeroed words after the last sample's region, so that its padding rows read this kernel's own data (words
 // of another kernel could hold anything, and a huge finite value times the zero weight it gets is not 0)
 constexpr int kMPad = ((32 * kQp > 32 * kTp ? 32 * kQp : 32 * kTp) - kMSample + 3) & ~3;
-constexpr float kLog2eRsqrtKq = 1.44269504088896341f * 0.316227766016838f;  // log2(e) / sqrt(10)
 #ifndef FRONT_MFMA_FAST_SOFTMAX  // 1: exp2 / rcp / * (1 / sqrt(10)); 0: the reference's steps (12% slower)
 #define FRONT_MFMA_FAST_SOFTMAX 1
 #endif

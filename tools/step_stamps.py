@@ -53,7 +53,8 @@ for i in range(a.steps):
     if i < a.steps - 1:
         env.reset(env.done, obs=obs, masks=masks)
 torch.cuda.synchronize()
-grid = (n + 31) // 32
+mpb = 16 if env.stride > 1024 else 32  # k_step's mazes per workgroup (kMPBig for layouts over 1 KB)
+grid = (n + mpb - 1) // mpb
 w = env.work[64:64 + 12 * grid].view(grid, 12).cpu().numpy().astype(np.int64)
 ph = w[:, :4]
 st5 = w[:, 6]
