@@ -436,12 +436,15 @@ int mm_actor_front_bwd(const float* ws, const float* x, int ldx, int B, int pari
  * MM_FRONT_BWD_VALU (mm_actor_front_bwd's): fp32 FMA, one lane per token;
  * MM_FRONT_BWD_MFMA: the per-sample products S = QK^T, dP = dctx V^T, dV, dK,
  * dQ on the fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fmaf chains; the faster:
- * 1.34 vs 1.59 ms at 419,430 rows; `grid` up to 3 per CU).  Same outputs and
+ * 1.22 vs 1.59 ms at 419,430 rows; `grid` from mm_actor_front_bwd_grid).  Same outputs and
  * partial layout; sums in a fixed order either way. */
 #define MM_FRONT_BWD_MFMA 0
 #define MM_FRONT_BWD_VALU 1
 int mm_actor_front_bwd_ex(const float* ws, const float* x, int ldx, int B, int parity, const float* dh,
                           float* partial, int grid, float* red, float* grad, int algo, void* stream);
+/* The persistent grid to pass as `grid` for B samples and `algo` (this build's
+ * workgroup shape and workgroups per CU of the current device), or MM_E_ARG. */
+int mm_actor_front_bwd_grid(int B, int algo);
 /* mm_actor_front_bwd_ex writing each parameter gradient straight into its
  * own buffer in the module's layout (the update's .grad storage): wproj_grad /
  * bproj_grad are HOST arrays of the 23 device pointers of the gradients of

@@ -849,9 +849,6 @@ __device__ __forceinline__ float xq_max(float v) {
     return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
-#ifndef FRONT_MFMA_PREFETCH
-#define FRONT_MFMA_PREFETCH 0  // 1: global operands loaded one sample / iteration ahead (measured slower)
-#endif
 
 // dP^T's B operand of one sample (dh row grow): rows 16 t + c16 (zero past token 22), columns 4 q4 .. 4 q4 + 3
 // and 16 + q4
@@ -877,6 +874,23 @@ constexpr int kTabS = kQkv * kPin + kQkv + 4;  // staged folded map per token: A
 // dctx unit, whose rows for all the iteration's samples are loaded up front (ef2_prefetch, before the barrier)
 static_assert(kEFR == 4, "k_front_bwd_mfma's E/F units are 4 rows");
 constexpr int kEF2G = kTok * kQkv / 4;  // 230 G units
+// samples per workgroup iteration (two per wavefront): 8 -> 256 threads, two E/F units for 89 of them, three
+// workgroups per CU (51 KB of LDS each).  12 -> 384 threads, every E/F unit its own thread (half the E/F
+// critical path), two workgroups per CU on LDS and registers -- measured 1.54x slower: a 6-wave workgroup
+// spreads its waves 2-2-1-1 over the SIMDs, and the second one then finds no SIMD pair free, so only one
+// workgroup per CU runs
+#ifndef FRONT_MFMA_ROWS
+#define FRONT_MFMA_ROWS 8
+#endif
+constexpr int kMRows = FRONT_MFMA_ROWS;
+constexpr int kMThreads = 32 * kMRows;
+constexpr int kMPerCU = kMRows == 12 ? 2 : 3;
+static_assert(kMRows == 8 || kMRows == 12, "FRONT_MFMA_ROWS is 8 or 12");
+constexpr int kMEFU = (kEFUnits + kMThreads - 1) / kMThreads;  // E/F units per thread (1 / 2)
+struct EFAccM {
+    f32x2 e[kMEFU][4][2];  // [unit][row a][column pair]
+    f32x2 s[kMEFU][2];     // [unit][row pair]
+};
 
 __device__ __forceinline__ void ef2_unit(int unit, int& tk, int& r0) {
     if (unit < kEF2G) {
@@ -888,53 +902,73 @@ __device__ __forceinline__ void ef2_unit(int unit, int& tk, int& r0) {
     }
 }
 
-__device__ __forceinline__ void ef2_prefetch(const float* __restrict__ dh0, int nrow, float4 (&fp)[kBwdRows]) {
-    const int fu = threadIdx.x < kEF2G ? threadIdx.x + kBwdThreads : threadIdx.x;
+// the dctx rows of samples g0 .. g0 + kEFPf - 1 (kEFPf at a time: 48 registers for 12 samples would cost the
+// third wave per SIMD)
+constexpr int kEFPf = kMRows == 12 ? 6 : kMRows;
+__device__ __forceinline__ void ef2_prefetch(const float* __restrict__ dh0, int nrow, int g0, float4 (&fp)[kEFPf]) {
+    const int fu = threadIdx.x < kEF2G ? threadIdx.x + kMThreads : threadIdx.x;
     int tk, r0;
     ef2_unit(fu, tk, r0);
     const bool has = fu < kEFUnits;
 #pragma unroll
-    for (int gg = 0; gg < kBwdRows; gg++)
-        fp[gg] = (has && gg < nrow) ? *reinterpret_cast<const float4*>(dh0 + (size_t)gg * kRowF + tk * kEmb + r0 - kQkv)
-                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < kEFPf; u++) {
+        const int gg = g0 + u;
+        fp[u] = (has && gg < nrow) ? *reinterpret_cast<const float4*>(dh0 + (size_t)gg * kRowF + tk * kEmb + r0 - kQkv)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
 template <int kStride, int kG, int kX>
-__device__ __forceinline__ void ef2_accumulate(const float* sm, int nrow, const float4 (&fp)[kBwdRows], EFAcc& acc) {
+__device__ __forceinline__ void ef2_accumulate(const float* sm, const float* __restrict__ dh0, int nrow,
+                                               float4 (&fp)[kEFPf], EFAccM& acc) {
 #pragma unroll
-    for (int u = 0; u < kEFU; u++) {
-        const int unit = threadIdx.x + u * kBwdThreads;
-        if (unit < kEFUnits) {
-            int tk, r0;
-            ef2_unit(unit, tk, r0);
-            const bool lds = unit < kEF2G;
+    for (int g0 = 0; g0 < kMRows; g0 += kEFPf) {
+        if (g0 > 0) ef2_prefetch(dh0, nrow, g0, fp);
 #pragma unroll
-            for (int gg = 0; gg < kBwdRows; gg++) {
-                if (gg < nrow) {
-                    const float* sg = sm + gg * kStride;
-                    const float4 gv = lds ? *reinterpret_cast<const float4*>(sg + kG + tk * kQkv + r0) : fp[gg];
-                    const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
-                    const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
-                    const f32x2 x01 = {xq.x, xq.y}, x23 = {xq.z, xq.w};
+        for (int u = 0; u < kMEFU; u++) {
+            const int unit = threadIdx.x + u * kMThreads;
+            if (unit < kEFUnits) {
+                int tk, r0;
+                ef2_unit(unit, tk, r0);
+                const bool lds = unit < kEF2G;
 #pragma unroll
-                    for (int a = 0; a < 4; a++) {
-                        const f32x2 ga = {gr[a], gr[a]};
-                        acc.e[u][a][0] = __builtin_elementwise_fma(ga, x01, acc.e[u][a][0]);
-                        acc.e[u][a][1] = __builtin_elementwise_fma(ga, x23, acc.e[u][a][1]);
+                for (int v = 0; v < kEFPf; v++) {
+                    const int gg = g0 + v;
+                    if (gg < nrow) {
+                        const float* sg = sm + gg * kStride;
+                        const float4 gv = lds ? *reinterpret_cast<const float4*>(sg + kG + tk * kQkv + r0) : fp[v];
+                        const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
+                        const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
+                        const f32x2 x01 = {xq.x, xq.y}, x23 = {xq.z, xq.w};
+#pragma unroll
+                        for (int a = 0; a < 4; a++) {
+                            const f32x2 ga = {gr[a], gr[a]};
+                            acc.e[u][a][0] = __builtin_elementwise_fma(ga, x01, acc.e[u][a][0]);
+                            acc.e[u][a][1] = __builtin_elementwise_fma(ga, x23, acc.e[u][a][1]);
+                        }
+#pragma unroll
+                        for (int a = 0; a < 2; a++) acc.s[u][a] += f32x2{gr[2 * a], gr[2 * a + 1]};
                     }
-#pragma unroll
-                    for (int a = 0; a < 2; a++) acc.s[u][a] += f32x2{gr[2 * a], gr[2 * a + 1]};
                 }
             }
         }
     }
 }
 
-__device__ __forceinline__ void ef2_write(float* partial, const EFAcc& acc) {
+__device__ __forceinline__ void ef2_zero(EFAccM& acc) {
+#pragma unroll
+    for (int u = 0; u < kMEFU; u++) {
+#pragma unroll
+        for (int a = 0; a < 4; a++) acc.e[u][a][0] = acc.e[u][a][1] = f32x2{0.f, 0.f};
+        acc.s[u][0] = acc.s[u][1] = f32x2{0.f, 0.f};
+    }
+}
+
+__device__ __forceinline__ void ef2_write(float* partial, const EFAccM& acc) {
     float* out = partial + (size_t)blockIdx.x * kPartLen;
 #pragma unroll
-    for (int u = 0; u < kEFU; u++) {
-        const int unit = threadIdx.x + u * kBwdThreads;
+    for (int u = 0; u < kMEFU; u++) {
+        const int unit = threadIdx.x + u * kMThreads;
         if (unit < kEFUnits) {
             int tk, r0;
             ef2_unit(unit, tk, r0);
@@ -948,49 +982,33 @@ __device__ __forceinline__ void ef2_write(float* partial, const EFAcc& acc) {
     }
 }
 
-__global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* __restrict__ ws,
+__global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_front_bwd_mfma(const float* __restrict__ ws,
                                                                    const float* __restrict__ x, int ldx, int B,
                                                                    int parity, const float* __restrict__ dh,
                                                                    float* __restrict__ partial) {
-    __shared__ __attribute__((aligned(16))) float sm[kBwdRows * kMSample + kMPad];
+    __shared__ __attribute__((aligned(16))) float sm[kMRows * kMSample + kMPad];
     __shared__ __attribute__((aligned(16))) float tab[kTok * kTabS];
     const int wave = threadIdx.x >> 6;
-    for (int e = threadIdx.x; e < kBwdRows * kMSample + kMPad; e += kBwdThreads) sm[e] = 0.f;  // (see kMSample)
+    for (int e = threadIdx.x; e < kMRows * kMSample + kMPad; e += kMThreads) sm[e] = 0.f;  // (see kMSample)
     // the folded maps once per workgroup (each lane's q|k|v reads them every iteration)
-    for (int e = threadIdx.x; e < kTok * (kQkv * kPin + kQkv); e += kBwdThreads) {
+    for (int e = threadIdx.x; e < kTok * (kQkv * kPin + kQkv); e += kMThreads) {
         const int t = e / (kQkv * kPin + kQkv), f = e % (kQkv * kPin + kQkv);
         tab[t * kTabS + f] = f < kQkv * kPin ? ws[kWsAT + t * kQkv * kPin + f] : ws[kWsC + t * kQkv + f - kQkv * kPin];
     }
-    EFAcc ef;
-    ef_zero(ef);
-    const int iters = (B + kBwdRows - 1) / kBwdRows;
+    EFAccM ef;
+    ef2_zero(ef);
+    const int iters = (B + kMRows - 1) / kMRows;
     const int tok = threadIdx.x & 31, hs = 2 * wave + ((threadIdx.x >> 5) & 1);
-    const int pc16 = threadIdx.x & 15, pq4 = (threadIdx.x >> 4) & 3;
-#if FRONT_MFMA_PREFETCH
-    // the next operands: this lane's x slice for phase 1 and the dP operands of the wave's next sample
-    float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ndf[2];
-    float ndt[2];
-    auto prefetch_iter = [&](int it2) {
-        const int r0 = it2 * kBwdRows, n2 = min(kBwdRows, B - r0);
-        if (it2 < iters && hs < n2 && tok < kTok) nx = xslice(x + (size_t)(r0 + hs) * ldx, tok, parity != 0);
-        if (it2 < iters && 2 * wave < n2) dp_operands(dh, r0 + 2 * wave, pc16, pq4, ndf, ndt);
-    };
-    prefetch_iter(blockIdx.x);
-#endif
     for (int it = blockIdx.x; it < iters; it += gridDim.x) {
-        const int row0 = it * kBwdRows;
-        const int nrow = min(kBwdRows, B - row0);
+        const int row0 = it * kMRows;
+        const int nrow = min(kMRows, B - row0);
         __syncthreads();  // previous iteration's reduction readers are done
         // ---- phase 1: lane (half h, token t) forms q|k|v of token t of sample 2 wave + h ----
         float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
         if (hs < nrow) {
             float4* q = reinterpret_cast<float4*>(sm + hs * kMSample + tok * kQp);
             if (tok < kTok) {
-#if FRONT_MFMA_PREFETCH
-                xv = nx;
-#else
                 xv = xslice(x + (size_t)(row0 + hs) * ldx, tok, parity != 0);
-#endif
                 float o[kQkv];
 #ifdef FRONT_DIAG_NO_P1LOAD  // timing diagnostic (wrong results): no folded-map table loads
 #pragma unroll
@@ -1023,10 +1041,7 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
             const float* QKV = my;
             float4 df[2];
             float dt[2];
-#if FRONT_MFMA_PREFETCH
-            df[0] = ndf[0], df[1] = ndf[1], dt[0] = ndt[0], dt[1] = ndt[1];
-            if (half == 0 && slot + 1 < nrow) dp_operands(dh, row0 + slot + 1, pc16, pq4, ndf, ndt);
-#elif defined(FRONT_DIAG_NO_DH)  // timing diagnostic (wrong results): no dh loads for dP
+#if defined(FRONT_DIAG_NO_DH)  // timing diagnostic (wrong results): no dh loads for dP
             df[0] = df[1] = make_float4(1.f, 2.f, 3.f, 4.f), dt[0] = dt[1] = 1.f;
 #else
             dp_operands(dh, row0 + slot, c16, q4, df, dt);
@@ -1225,16 +1240,13 @@ __global__ __launch_bounds__(kBwdThreads, 3) void k_front_bwd_mfma(const float* 
                     }
                 }
         }
-        float4 fp[kBwdRows];
-        ef2_prefetch(dh + (size_t)row0 * kRowF, nrow, fp);
+        float4 fp[kEFPf];
+        ef2_prefetch(dh + (size_t)row0 * kRowF, nrow, 0, fp);
         // the X rows (the reduction's x operand; phase 1's lanes hold them), now that both samples' QKV words are dead
         if (hs < nrow && tok < kTok) *reinterpret_cast<float4*>(sm + hs * kMSample + kMX + tok * kPin) = xv;
-#if FRONT_MFMA_PREFETCH
-        prefetch_iter(it + gridDim.x);  // in flight during the E/F phase
-#endif
         __syncthreads();
 #ifndef FRONT_DIAG_NO_EF  // timing diagnostic (wrong results): no E/F accumulation
-        ef2_accumulate<kMSample, kMG, kMX>(sm, nrow, fp, ef);
+        ef2_accumulate<kMSample, kMG, kMX>(sm, dh + (size_t)row0 * kRowF, nrow, fp, ef);
 #endif
     }
     ef2_write(partial, ef);
@@ -1327,7 +1339,27 @@ using namespace mm;
 
 extern "C" int mm_actor_front_ws_len(void) { return kWsLen; }
 extern "C" int mm_actor_front_grad_len(void) { return kGradLen; }
+static int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+    return cus[dev];
+}
+
 extern "C" int mm_actor_front_partial_len(void) { return kPartLen; }
+
+// the persistent grid of the backward for B samples: every workgroup resident at once (MFMA kernel: kMRows
+// samples per iteration, kMPerCU workgroups per CU; VALU kernel: 8 samples, two per CU)
+extern "C" int mm_actor_front_bwd_grid(int B, int algo) {
+    if (B < 0 || (algo != MM_FRONT_BWD_MFMA && algo != MM_FRONT_BWD_VALU)) return MM_E_ARG;
+    const int rows = algo == MM_FRONT_BWD_MFMA ? kMRows : kBwdRows;
+    const int per_cu = algo == MM_FRONT_BWD_MFMA ? kMPerCU : 2;
+    const int groups = (B + rows - 1) / rows;
+    const int cap = per_cu * cu_count();
+    return groups < 1 ? 1 : (groups < cap ? groups : cap);
+}
 
 extern "C" int mm_actor_front_prep(const float* const* wproj, const float* const* bproj, const float* wq,
                                    const float* wk, const float* wv, float* ws, void* stream) {
@@ -1342,14 +1374,6 @@ extern "C" int mm_actor_front_prep(const float* const* wproj, const float* const
     return (int)hipGetLastError();
 }
 
-static int cu_count() {
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus[dev] = 256;
-    return cus[dev];
-}
 
 extern "C" int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, int B, int parity, float* h,
                                      int algo, void* stream) {
@@ -1380,7 +1404,7 @@ static int front_bwd(const float* ws, const float* x, int ldx, int B, int parity
     if (algo != MM_FRONT_BWD_MFMA && algo != MM_FRONT_BWD_VALU) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
     if (algo == MM_FRONT_BWD_MFMA)
-        hipLaunchKernelGGL(k_front_bwd_mfma, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
+        hipLaunchKernelGGL(k_front_bwd_mfma, dim3(grid), dim3(kMThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
     else
         hipLaunchKernelGGL(k_front_bwd, dim3(grid), dim3(kBwdThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
     hipError_t e = hipGetLastError();

@@ -37,14 +37,14 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample", "mm_head_sample_ex",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd", "mm_actor_front_fwd_ex",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd", "mm_actor_front_bwd_ex",
-           "mm_actor_front_bwd_to",
+           "mm_actor_front_bwd_to", "mm_actor_front_bwd_grid",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
            "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
            "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
            "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi")
-VERSION = 301  # mm_version() this binding is written for
+VERSION = 302  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
@@ -201,6 +201,8 @@ def lib():
         L.mm_actor_front_fwd_ex.restype = i32
         L.mm_actor_front_grad_len.restype = i32
         L.mm_actor_front_partial_len.restype = i32
+        L.mm_actor_front_bwd_grid.argtypes = [i32, i32]
+        L.mm_actor_front_bwd_grid.restype = i32
         L.mm_actor_front_bwd.argtypes = [P, P, i32, i32, i32, P, P, i32, P, P, P]
         L.mm_actor_front_bwd.restype = i32
         L.mm_actor_front_bwd_ex.argtypes = [P, P, i32, i32, i32, P, P, i32, P, P, i32, P]

@@ -87,10 +87,15 @@ FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "mfma")
 
 
 def _front_bwd_grid(B, dev):
-    """Persistent grid of the front-end backward: 8-sample workgroups, two per CU (VALU kernel, 63 KB of
-    LDS) or three (MFMA kernel, 51 KB)."""
-    per_cu = 3 if FRONT_BWD_ALGO == "mfma" else 2
-    return max(1, min(per_cu * _cu_count(dev), (B + 7) // 8))
+    """Persistent grid of the front-end backward (mm_actor_front_bwd_grid: 8-sample workgroups, three per CU
+    for the MFMA kernel, two for the VALU kernel)."""
+    from . import _lib
+
+    with torch.cuda.device(dev):
+        grid = _lib.lib().mm_actor_front_bwd_grid(int(B), _lib.FRONT_BWD[FRONT_BWD_ALGO])
+    if grid < 1:
+        raise _lib.MMError(f"mm_actor_front_bwd_grid failed with status {grid}")
+    return grid
 # the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads) or "row1" (one per lane);
 # bit-identical outputs (csrc/actor_front.hip k_front_fwd2 / k_front_fwd)
 FRONT_FWD_ALGO = _os.environ.get("MARLMAZE_FRONT_FWD", "row1")
