@@ -39,11 +39,10 @@ s = torch.cuda.current_stream()
 
 def one(i, ev=None):
     ops.sample(ml, kl, masks.view(2 * n, 6), seed=1, offset=i, actions=acts)
-    if ev:
-        ev[0].record(s)
-    env.step(acts.view(n, 2, 2), auto_reset=2, obs=obs, masks=masks)  # finished mazes queued (done list)
-    if ev:
-        ev[1].record(s)
+    # the step kernel's duration from events stamped at its own start and end (mm_env_step_timed): stream
+    # events around the launch would also hold the host's launch gaps of this Python loop
+    env.step(acts.view(n, 2, 2), auto_reset=2, obs=obs, masks=masks,
+             events=(ev[0], ev[1]) if ev else None)  # finished mazes queued (done list)
     env.reset_done(obs=obs, masks=masks)  # PPO.get_batch's reset (PPO.py:127-130); next mazes pre-generated
     if ev:
         ev[2].record(s)
@@ -53,6 +52,10 @@ for i in range(a.warmup):
     one(i)
 torch.cuda.synchronize()
 evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(a.steps)]
+for e in evs:  # mm_env_step_timed takes events recorded once already
+    e[0].record(s)
+    e[1].record(s)
+torch.cuda.synchronize()
 t0 = time.time()
 for i in range(a.steps):
     one(a.warmup + i, evs[i])
