@@ -1089,19 +1089,18 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                         dP[J][I] = mfma4(vt[J], dt[I], acc);
                     }
             }
-            // operands of dK (B: q of rows i = 16 t + 4 q4 + e, column c16) and dQ^T (A: k of rows
-            // j = 16 t + 4 q4 + e, column c16), from the zero pads for c16 >= 10; read before the QKV words
-            // are reused
-            // (dK's k = i runs over 16 + q4 + 4 e for the second half: two steps cover i < 24)
-            float qb[kKH], ka[2][4];
+            // operands of dK (B: q of rows i = kh_row(s, q4), column c16) and dQ^T (A: k of rows j = kh_row(s, q4),
+            // column c16; 0 for the padding token 23, whose dS^T row in T is never written), from the zero pads for
+            // c16 >= 10; read before the QKV words are reused
+            float qb[kKH], ka[kKH];
             {
                 const int ca = min(c16, kKq);
 #pragma unroll
-                for (int t = 0; t < 2; t++)
-#pragma unroll
-                    for (int e = 0; e < 4; e++) ka[t][e] = QKV[(16 * t + 4 * q4 + e) * kQp + kKO + ca];
-#pragma unroll
-                for (int s = 0; s < kKH; s++) qb[s] = QKV[kh_row(s, q4) * kQp + kQO + ca];
+                for (int s = 0; s < kKH; s++) {
+                    const int r = kh_row(s, q4);
+                    qb[s] = QKV[r * kQp + kQO + ca];
+                    ka[s] = r < kTok ? QKV[r * kQp + kKO + ca] : 0.f;
+                }
             }
             // ---- softmax over j per query column i, then dS^T = P (dP - rowsum(P dP)) / sqrt(10) in place
             // of dP^T; padding rows j (k = 0, so S = 0) are kept out of the max and the sum.  exp2 / rcp
@@ -1162,14 +1161,6 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             }
             f32x4_t (&P)[2][2] = S;
             f32x4_t (&dS)[2][2] = dP;
-            // ---- dQ^T = K^T dS^T: rows a = 4 q4 + g (10 of 16), columns i; B = the dS^T tiles ----
-            f32x4_t dQ[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-            for (int J = 0; J < 2; J++)
-#pragma unroll
-                for (int g = 0; g < 4; g++)
-#pragma unroll
-                    for (int I = 0; I < 2; I++) dQ[I] = mfma4(ka[J][g], dS[J][I][g], dQ[I]);
             wave_sync();  // the QKV words are dead: the transpose buffer (rows j < 23)
             float* T = my;
             // ---- dV = P^T dctx: rows j, columns c (20 -> 32); k = i = 16 ib + 4 q4 + e ----
@@ -1210,13 +1201,18 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                     for (int g = 0; g < 4; g++)
                         if (16 * J + 4 * q4 + g < kTok) T[(16 * J + 4 * q4 + g) * kTp + 16 * I + c16] = dS[J][I][g];
             wave_sync();
-            // ---- dK = dS^T Q: rows j, columns a (10 of 16); k = i = 16 ib + 4 q4 + e ----
+            // ---- dK = dS^T Q: rows j, columns a (10 of 16); k = i = kh_row(s, q4) ----
+            // ---- dQ^T = K^T dS^T: rows a = 4 q4 + g (10 of 16), columns i; k = j = kh_row(s, q4): B = dS^T rows
+            // j from T (six steps over j < 24 instead of eight over the accumulator tiles' j < 32) ----
             f32x4_t dK[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+            f32x4_t dQ[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int s = 0; s < kKH; s++) {
                 const int i = kh_row(s, q4);
 #pragma unroll
                 for (int J = 0; J < 2; J++) dK[J] = mfma4(T[(16 * J + c16) * kTp + i], qb[s], dK[J]);
+#pragma unroll
+                for (int I = 0; I < 2; I++) dQ[I] = mfma4(ka[s], T[i * kTp + 16 * I + c16], dQ[I]);
             }
             wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
 #pragma unroll

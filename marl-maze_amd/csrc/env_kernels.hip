@@ -540,7 +540,12 @@ __device__ __forceinline__ void get_replay(const int4* r, Agent& s, int& qflags,
     vis.vad = w3.x;
 }
 
-template <int MPB>
+// LAT (latency form, chosen when the grid is at most two workgroups per CU: one round, one wavefront per
+// SIMD, so the launch is the per-maze critical chain): every lane replays both agents itself, in the
+// reference's order, instead of handing the two replays between the wavefronts (two barriers and two LDS
+// records); and in the 16-maze workgroups of layouts over 1 KB the otherwise idle upper half of each
+// wavefront takes one of the lane's two relative directions, so each lane summarises one ray, not two
+template <int MPB, bool LAT>
 __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_t* __restrict__ act,
                                                         float* __restrict__ obs, uint8_t* __restrict__ masks,
                                                         float* __restrict__ reward, uint8_t* __restrict__ done,
@@ -554,11 +559,14 @@ __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_
     // maze l >> 1, agent l & 1.  h is wavefront-uniform, so each wavefront
     // computes only its half of the observation.
     const int h = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lm = (threadIdx.x & 63) >> 1;  // maze within the workgroup
+    constexpr bool kDSplit = LAT && MPB == kMPBig;  // upper half-wavefront: the lane's second direction
+    const int lm = kDSplit ? (threadIdx.x & 31) >> 1 : (threadIdx.x & 63) >> 1;  // maze within the workgroup
+    const int dsl = kDSplit ? (threadIdx.x >> 5) & 1 : 0;
     const int a = threadIdx.x & 1;
-    const bool lead = h == 0 && a == 0;  // writes the maze's marks and state to HBM
+    const bool lead = h == 0 && a == 0 && dsl == 0;  // writes the maze's marks and state to HBM
     const int m = m0 + lm;
-    const bool valid = lm < nb;
+    const bool valid0 = lm < nb;     // moves and direction summaries (both half-wavefronts when kDSplit)
+    const bool valid = valid0 && dsl == 0;
 #ifdef MM_STEP_STAMPS  // tools/step_stamps.py: per-workgroup phase clocks into work[64 + 12*block]
     uint64_t st[10];
     st[0] = __builtin_amdgcn_s_memtime();
@@ -573,7 +581,7 @@ __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_
     mm_maze_t mz{};
     mm_agent_t g0{}, g1{};
     char4 ac{};
-    if (valid) {
+    if (valid0) {
         mz = env.mazes[m];
         g0 = env.agents[2 * m];
         g1 = env.agents[2 * m + 1];
@@ -589,7 +597,7 @@ __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_
     Agent a1 = load_agent(g1, 3);
     uint32_t status = mz.status;
     int first_key = 0, have_key = 0;
-    if (valid) {
+    if (valid0) {
         // maze.py:75-90: both wavefronts replay the moves and write the same
         // mark bytes into LDS; the lead lane also writes them to HBM
         uint8_t* gl = lead ? env.layout + (size_t)m * stride : nullptr;
@@ -606,11 +614,16 @@ __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_
     MM_STAMP(5);
     // direction summaries of the maze, [agent][relative direction]
     uint32_t* ssum = reinterpret_cast<uint32_t*>(smem + step_sum_off<MPB>(stride)) + 8 * lm;
-    if (valid) {  // geometry of this lane's two directions of agent a
+    if (valid0) {  // geometry of this lane's two directions of agent a (kDSplit: its one direction)
         const Agent me0 = a ? a1 : a0, ot0 = a ? a0 : a1;
-        const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
-        const uint32_t sB = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + 1, me0.tag, ot0.x, ot0.y, true);
-        *reinterpret_cast<uint2*>(ssum + 4 * a + 2 * h) = make_uint2(sA, sB);
+        if constexpr (kDSplit) {
+            ssum[4 * a + 2 * h + dsl] =
+                summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + dsl, me0.tag, ot0.x, ot0.y, true);
+        } else {
+            const uint32_t sA = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h, me0.tag, ot0.x, ot0.y, true);
+            const uint32_t sB = summarize_dir(v, me0.x, me0.y, me0.dir, 2 * h + 1, me0.tag, ot0.x, ot0.y, true);
+            *reinterpret_cast<uint2*>(ssum + 4 * a + 2 * h) = make_uint2(sA, sB);
+        }
     }
     __syncthreads();
     MM_STAMP(6);
@@ -624,27 +637,36 @@ __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_
     // The two replays form a chain: wavefront 0 replays agent 0, wavefront 1
     // then replays agent 1, and each hands its result to the other through
     // LDS (one record per replay and maze), so every replay runs once.
-    int4* xrec = reinterpret_cast<int4*>(smem + step_xchg_off<MPB>(stride)) + 8 * lm;  // [replay][4 x int4]
     Vis r0{0, 0, 0}, r1{0, 0, 0};
-    if (valid && h == 0) {
-        r0 = replay(v, a0, a1, sum0);
-        if (a == 0) put_replay(xrec, a0, a1.flags, r0);
-    }
-    __syncthreads();
-    Agent a0_obs = a0;  // agent 0's observation is taken here, before agent 1 may update it
-    if (valid && h == 1) {
-        int f1 = a1.flags;
-        get_replay(xrec, a0, f1, r0);
-        a1.flags = f1;
+    Agent a0_obs = a0;  // agent 0's observation is taken after its replay, before agent 1 may update it
+    if constexpr (LAT) {  // both replays in every lane, in order (no hand-offs)
+        if (valid) {
+            r0 = replay(v, a0, a1, sum0);
+            a0_obs = a0;
+            r1 = replay(v, a1, a0, sum1);
+        }
+    } else {
+        int4* xrec = reinterpret_cast<int4*>(smem + step_xchg_off<MPB>(stride)) + 8 * lm;  // [replay][4 x int4]
+        if (valid && h == 0) {
+            r0 = replay(v, a0, a1, sum0);
+            if (a == 0) put_replay(xrec, a0, a1.flags, r0);
+        }
+        __syncthreads();
         a0_obs = a0;
-        r1 = replay(v, a1, a0, sum1);
-        if (a == 0) put_replay(xrec + 4, a1, a0.flags, r1);
-    }
-    __syncthreads();
-    if (valid && h == 0) {
-        int f0 = a0.flags;
-        get_replay(xrec + 4, a1, f0, r1);
-        a0.flags = f0;
+        if (valid && h == 1) {
+            int f1 = a1.flags;
+            get_replay(xrec, a0, f1, r0);
+            a1.flags = f1;
+            a0_obs = a0;
+            r1 = replay(v, a1, a0, sum1);
+            if (a == 0) put_replay(xrec + 4, a1, a0.flags, r1);
+        }
+        __syncthreads();
+        if (valid && h == 0) {
+            int f0 = a0.flags;
+            get_replay(xrec + 4, a1, f0, r1);
+            a0.flags = f0;
+        }
     }
     const bool exit_ready = a0_obs.f(MM_AF_TEAM_KEY) && a0_obs.f(MM_AF_KNOWS_END) && a1.f(MM_AF_TEAM_KEY) &&
                             a1.f(MM_AF_KNOWS_END);
@@ -750,6 +772,16 @@ inline size_t step_lds_bytes(int stride) {
     return sums_end > xchg_end ? sums_end : xchg_end;
 }
 
+// compute units of the current device (cached per device)
+static int cu_count() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus[dev] = 256;
+    return cus[dev];
+}
+
 inline int check_env(const mm_env_t* env) {
     if (!env || env->n <= 0 || !env->layout || !env->agents || !env->mazes || !env->rng || !env->work) return MM_E_ARG;
     const int need = mm_layout_stride(env->size_w, env->size_h, env->rand_sizes, env->rand_lo, env->rand_hi);
@@ -820,15 +852,27 @@ extern "C" int mm_env_step_timed(const mm_env_t* env, const int8_t* actions, flo
     hipStream_t s = (hipStream_t)stream;
     // hipExtLaunchKernel stamps the events at the kernel's own start / end
     if (env->layout_stride > kMPBigStride) {
+        const int grid = (env->n + kMPBig - 1) / kMPBig;
         const size_t lds = step_lds_bytes<kMPBig>(env->layout_stride);
-        hipExtLaunchKernelGGL(k_step<kMPBig>, dim3((env->n + kMPBig - 1) / kMPBig), dim3(kStepThreads),
-                              (uint32_t)lds, s, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, *env, actions, obs,
-                              masks, reward, done, ep_stats, auto_reset ? 1 : 0);
+        if (grid <= 2 * cu_count())
+            hipExtLaunchKernelGGL((k_step<kMPBig, true>), dim3(grid), dim3(kStepThreads), (uint32_t)lds, s,
+                                  (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, *env, actions, obs, masks, reward,
+                                  done, ep_stats, auto_reset ? 1 : 0);
+        else
+            hipExtLaunchKernelGGL((k_step<kMPBig, false>), dim3(grid), dim3(kStepThreads), (uint32_t)lds, s,
+                                  (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, *env, actions, obs, masks, reward,
+                                  done, ep_stats, auto_reset ? 1 : 0);
     } else {
+        const int grid = (env->n + 2 * kMPBig - 1) / (2 * kMPBig);
         const size_t lds = step_lds_bytes<2 * kMPBig>(env->layout_stride);
-        hipExtLaunchKernelGGL(k_step<2 * kMPBig>, dim3((env->n + 2 * kMPBig - 1) / (2 * kMPBig)),
-                              dim3(kStepThreads), (uint32_t)lds, s, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0,
-                              *env, actions, obs, masks, reward, done, ep_stats, auto_reset ? 1 : 0);
+        if (grid <= 2 * cu_count())
+            hipExtLaunchKernelGGL((k_step<2 * kMPBig, true>), dim3(grid), dim3(kStepThreads), (uint32_t)lds, s,
+                                  (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, *env, actions, obs, masks, reward,
+                                  done, ep_stats, auto_reset ? 1 : 0);
+        else
+            hipExtLaunchKernelGGL((k_step<2 * kMPBig, false>), dim3(grid), dim3(kStepThreads), (uint32_t)lds, s,
+                                  (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, *env, actions, obs, masks, reward,
+                                  done, ep_stats, auto_reset ? 1 : 0);
     }
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;

@@ -191,6 +191,33 @@ def test_65536_mazes_10x10_match_oracle():
         masks = om
 
 
+def test_big_layouts_both_step_forms_match_oracle():
+    """The env-step kernel has a latency form (grid <= 2 workgroups per CU: every lane replays both agents,
+    and 20x20 layouts split each lane's two directions over the half-wavefronts) and a throughput form
+    (the replays handed between the wavefronts).  The random-play tests run small batches (latency form);
+    here 20x20 mazes above 2 x 256 CUs x 16 mazes per workgroup take the throughput form, with resets."""
+    n, steps = 9000, 40
+    cfg = dict(default_size=(20, 20), max_timestep=30)
+    seeds = np.arange(n, dtype=np.uint64) * np.uint64(31) + np.uint64(5)
+    env = VecMaze(n, seeds=seeds, **cfg)
+    ora = OracleEnv(n, seeds=seeds, **cfg)
+    go, gm = env.reset()
+    oo, om = ora.reset_all()
+    assert np.array_equal(go.cpu().numpy(), oo)
+    rng = np.random.default_rng(9)
+    masks = om
+    for s in range(steps):
+        act = random_legal(rng, masks)
+        go, gm, gr, gd = env.step(torch.as_tensor(act).cuda(), auto_reset=True)
+        oo, om, orw, od = ora.step_all(act, auto_reset=True)
+        assert np.array_equal(go.cpu().numpy(), oo), s
+        assert np.array_equal(gm.cpu().numpy().astype(bool), om), s
+        assert np.array_equal(gr.cpu().numpy(), orw) and np.array_equal(gd.cpu().numpy().astype(bool), od), s
+        masks = om
+    for i in range(0, n, 997):
+        assert np.array_equal(env.agent_state(i), np.stack([ora.agent(i, a) for a in range(2)])), i
+
+
 def test_reset_mask_and_independence():
     """Resetting a subset leaves the other mazes untouched; per-maze streams are
     independent of the batch they live in (seed i behaves the same alone)."""
