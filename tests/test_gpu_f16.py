@@ -14,7 +14,8 @@ unit roundoff 2^-11 = 4.9e-4 per operand (measured values in brackets):
   each parameter's gradient ||g - g64|| <= 5e-3 ||g64|| [<= 1.5e-3] and the
   cosine with the exact gradient >= 0.9999 [0.999999];
 * configs[4]'s per-GPU share (32,768 mazes): rollout + the whole update run,
-  losses finite, same episode statistics machinery as fp32.
+  losses finite; one full-size minibatch (209,714 actor rows) of that rollout
+  held to the gradient bar above against the fp32-class engine.
 """
 import copy
 
@@ -104,11 +105,40 @@ def test_f16_minibatch_gradients_vs_fp64_oracle(golden):
 
 def test_f16_config4_per_gpu_share():
     """BASELINE configs[4] on one GPU: 32,768 mazes (262,144 / 8), 10x10, one
-    rollout (T=16) and the reference update (5 x 5 minibatches)."""
+    rollout (T=16) and the reference update (5 x 5 minibatches).  Before the
+    update, one full-size minibatch (a fifth of the 524,288 rollout samples:
+    209,714 actor rows) is held to the same gradient bar as the 32,768-sample
+    case above, against the fp32-class engine (PPO dtype "f32", itself held to
+    the fp64 oracle at 1e-5 in test_gpu_update_parity.py) at the same
+    parameters: the oracle is too slow for this size."""
     n, T = 32768, 16
     ag = _agent(n_envs=n, horizon=T, batch_size=n * T, epochs=1, sample_seed=4,
                 env_config=dict(default_size=(10, 10), max_timestep=1200, seed_base=0))
-    ag.train()
+    b_obs, b_act, b_lp, _, _, b_masks, b_advs, b_vals = ag.get_batch()
+    mb = b_obs.shape[0] // 5
+    adv = (b_advs - b_advs.mean()) / (b_advs.std() + 1e-10)
+    batch = (b_obs[:mb], b_act[:mb], b_lp[:mb], adv[:mb], (b_advs + b_vals)[:mb], b_masks[:mb])
+    ref = _agent(n_envs=64, dtype="f32")
+    ref.actor.load_state_dict(ag.actor.state_dict())
+    ref.critic.load_state_dict(ag.critic.state_dict())
+    al, cl = ag.minibatch_grads(*batch)
+    ral, rcl = ref.minibatch_grads(*batch)
+    assert abs(float(al) - float(ral)) <= 1e-3 * abs(float(ral)) + 1e-5, (float(al), float(ral))
+    assert abs(float(cl) - float(rcl)) <= 1e-3 * abs(float(rcl)) + 1e-5, (float(cl), float(rcl))
+    worst = []
+    for net, rnet in ((ag.actor, ref.actor), (ag.critic, ref.critic)):
+        rg = dict(rnet.named_parameters())
+        for k, p in net.named_parameters():
+            g, r = p.grad.detach().double().flatten(), rg[k].grad.detach().double().flatten()
+            rel = (g - r).norm().item() / max(r.norm().item(), 1e-30)
+            cos = torch.dot(g, r).item() / max(g.norm().item() * r.norm().item(), 1e-30)
+            worst.append((rel, cos, k))
+    worst.sort(reverse=True)
+    print("f16 full-size minibatch, worst gradient tensors:", [(f"{r:.2e}", f"{c:.6f}", k) for r, c, k in worst[:4]])
+    assert all(rel <= 5e-3 and cos >= 0.9999 for rel, cos, _ in worst), worst[:4]
+    del ref
+    hist = ag.update(b_obs, b_act, b_lp, b_masks, b_advs, b_vals)
+    ag.history.append(dict(actor_loss=float(hist[-1, 0]), critic_loss=float(hist[-1, 1])))
     h = ag.history[-1]
     assert np.isfinite([h["actor_loss"], h["critic_loss"]]).all()
     assert all(torch.isfinite(p).all() for p in list(ag.actor.parameters()) + list(ag.critic.parameters()))
