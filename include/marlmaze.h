@@ -398,6 +398,12 @@ int mm_head_sample_ex(const float* h, int ldh, int K, const float* w, const floa
                       uint64_t seed, uint64_t offset, const uint64_t* offset_dev, int8_t* actions, float* logp,
                       float* joint_logp, float* logits, void* stream);
 
+/* The heads alone (the update's forward; networks.py:38-41): logits [M, 6] =
+ * h W^T + b with mm_head_sample's arithmetic per row, so the logits equal the
+ * ones mm_head_sample computes for the same rows.  Same operand rules (K % 4 ==
+ * 0, K <= 1024, 16-byte aligned rows); M * ldh * 4 < 2^31. */
+int mm_heads_fwd(const float* h, int ldh, int K, const float* w, const float* b, int M, float* logits, void* stream);
+
 /* Actor front-end, fused (networks.py:31-34,51-82): the 23 feature embeddings
  * (Projection; parity != 0 keeps quirk Q1, every embedding reads x[:, 0:d_i]),
  * Q/K/V, softmax(QK^T/sqrt(10))V and the residual.

@@ -804,7 +804,7 @@ inline int check_env(const mm_env_t* env) {
 
 using namespace mm;
 
-extern "C" int mm_version(void) { return 302; }
+extern "C" int mm_version(void) { return 303; }
 
 extern "C" int mm_env_desc_size(void) { return (int)sizeof(mm_env_t); }
 

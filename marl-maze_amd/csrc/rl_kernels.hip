@@ -377,6 +377,88 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* 
     if (joint && valid && j == 0 && (row & 1) == 0) joint[row >> 1] = lp + (row + 1 < M ? other : 0.f);
 }
 
+// The heads alone (the update's forward, networks.py:38-41): logits [M, 6] = h W^T + b with k_head_sample's
+// arithmetic per row -- the same lanes, per-lane fma order and butterfly -- so the update's logits equal the
+// rollout's bit for bit at the same parameters (the PPO ratio is exactly 1 before the first step).  A
+// streaming GEMV (443 MB of h per 419,430-row minibatch): NS (= ceil(K / 32)) 16-byte loads per lane all in
+// flight, through a buffer resource (columns past K and rows past M read zeros: no exec-masked loads), head
+// weights zero-padded in LDS.  NS = 0: a runtime loop for other widths.
+template <int NS>
+__global__ __launch_bounds__(kHsLanes* kHsRows) void k_heads_fwd(const float* __restrict__ h, int ldh, int K,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ b, int M,
+                                                                 float* __restrict__ logits) {
+    constexpr int kSpan = NS > 0 ? 32 * NS : kHsMaxK;  // W row pitch (zero past K)
+    __shared__ __attribute__((aligned(16))) float W[6 * kSpan];
+    constexpr int kB = 8;
+    for (int e0 = threadIdx.x; e0 < 6 * kSpan; e0 += kB * blockDim.x) {
+        float t[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int e = e0 + u * blockDim.x, o = e / kSpan, c = e - o * kSpan;
+            t[u] = (e < 6 * kSpan && c < K) ? w[o * K + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int e = e0 + u * blockDim.x;
+            if (e < 6 * kSpan) W[e] = t[u];
+        }
+    }
+    __syncthreads();
+    const int j = threadIdx.x % kHsLanes;
+    const int row = blockIdx.x * kHsRows + threadIdx.x / kHsLanes;
+    float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (NS > 0) {
+        // gfx9 buffer resource word 3 0x00020000: 32-bit data format, raw addressing
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)h, (short)0, (int)((size_t)M * ldh * 4), 0x00020000);
+        float4 hv[NS];
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int c = 4 * j + 32 * s;
+            const uint32_t off = (row < M && c < K) ? 4u * ((uint32_t)row * (uint32_t)ldh + (uint32_t)c) : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+            hv[s] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                __uint_as_float(v[3]));
+        }
+#pragma unroll
+        for (int s = 0; s < NS; s++) {
+            const int c = 4 * j + 32 * s;
+#pragma unroll
+            for (int o = 0; o < 6; o++) {
+                const float4 wv = *reinterpret_cast<const float4*>(W + o * kSpan + c);
+                acc[o] = fmaf(hv[s].x, wv.x, acc[o]);
+                acc[o] = fmaf(hv[s].y, wv.y, acc[o]);
+                acc[o] = fmaf(hv[s].z, wv.z, acc[o]);
+                acc[o] = fmaf(hv[s].w, wv.w, acc[o]);
+            }
+        }
+    } else if (row < M) {
+        const float* hr = h + (size_t)row * ldh;
+        for (int c = 4 * j; c < K; c += 4 * kHsLanes) {
+            const float4 hv = *reinterpret_cast<const float4*>(hr + c);
+#pragma unroll
+            for (int o = 0; o < 6; o++) {
+                const float4 wv = *reinterpret_cast<const float4*>(W + o * kSpan + c);
+                acc[o] = fmaf(hv.x, wv.x, acc[o]);
+                acc[o] = fmaf(hv.y, wv.y, acc[o]);
+                acc[o] = fmaf(hv.z, wv.z, acc[o]);
+                acc[o] = fmaf(hv.w, wv.w, acc[o]);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 0; o < 6; o++) {
+#pragma unroll
+        for (int d = kHsLanes / 2; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+    }
+    // lane j < 6 of the row writes logit j: a row's 24 bytes, the workgroup's 32 rows contiguous
+    float v = acc[0];
+#pragma unroll
+    for (int o = 1; o < 6; o++) v = j == o ? acc[o] : v;
+    if (row < M && j < 6) logits[(size_t)row * 6 + j] = v + b[j];
+}
+
 // per agent row: log pi(a | z) for the masked move logits z[0:5] and the
 // masked mark logit z[5] (PPO.py:154-168, torch's op order in fp32); also the
 // gradient d log pi / d z when grad != null
@@ -529,6 +611,20 @@ extern "C" int mm_head_sample(const float* h, int ldh, int K, const float* w, co
                               float* logits, void* stream) {
     return mm_head_sample_ex(h, ldh, K, w, b, masks, M, seed, offset, nullptr, actions, logp, joint_logp, logits,
                              stream);
+}
+
+extern "C" int mm_heads_fwd(const float* h, int ldh, int K, const float* w, const float* b, int M, float* logits,
+                            void* stream) {
+    if (!h || !w || !b || !logits || M < 0 || K <= 0 || (K & 3) || K > kHsMaxK || ldh < K || (ldh & 3) ||
+        ((uintptr_t)h & 15) || (size_t)M * ldh * 4 >= 0x80000000ull)
+        return MM_E_ARG;
+    if (M == 0) return 0;
+    const dim3 grid((M + kHsRows - 1) / kHsRows), block(kHsLanes * kHsRows);
+    if ((K + 31) / 32 == 9)  // the actor's 264-wide last hidden layer
+        hipLaunchKernelGGL(k_heads_fwd<9>, grid, block, 0, (hipStream_t)stream, h, ldh, K, w, b, M, logits);
+    else
+        hipLaunchKernelGGL(k_heads_fwd<0>, grid, block, 0, (hipStream_t)stream, h, ldh, K, w, b, M, logits);
+    return (int)hipGetLastError();
 }
 
 extern "C" int mm_ppo_loss_partials(int M) { return (M + kLossThreads - 1) / kLossThreads; }

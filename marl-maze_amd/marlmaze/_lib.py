@@ -34,7 +34,7 @@ AF_HAS_MARK = 64
 
 # exported symbols (tests check every one of them is present)
 EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", "mm_env_reset",
-           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample", "mm_head_sample_ex",
+           "mm_env_step", "mm_env_step_timed", "mm_env_reset_done", "mm_env_pregen", "mm_gae", "mm_gae_ex", "mm_sample", "mm_head_sample", "mm_head_sample_ex", "mm_heads_fwd",
            "mm_actor_front_ws_len", "mm_actor_front_prep", "mm_actor_front_fwd", "mm_actor_front_fwd_ex",
            "mm_actor_front_grad_len", "mm_actor_front_partial_len", "mm_actor_front_bwd", "mm_actor_front_bwd_ex",
            "mm_actor_front_bwd_to", "mm_actor_front_bwd_grid",
@@ -44,7 +44,7 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
            "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
            "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi")
-VERSION = 302  # mm_version() this binding is written for
+VERSION = 303  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
@@ -132,6 +132,8 @@ def lib():
         L.mm_sample.restype = i32
         L.mm_head_sample.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P]
         L.mm_head_sample.restype = i32
+        L.mm_heads_fwd.argtypes = [P, i32, i32, P, P, i32, P, P]
+        L.mm_heads_fwd.restype = i32
         L.mm_head_sample_ex.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P, P]
         L.mm_head_sample_ex.restype = i32
         L.mm_x3_tp_len.argtypes = [i32, i32]

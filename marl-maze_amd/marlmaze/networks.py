@@ -252,10 +252,21 @@ def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None):
 
 
 def _heads_fwd(h, wh, bh):
-    """The heads (networks.py:38-41) at x3 precision (see above)."""
-    from . import x3
+    """The heads (networks.py:38-41): mm_heads_fwd, fp32 FMA per row with mm_head_sample's arithmetic (the
+    rollout's logits, bit for bit), a streaming GEMV over h.  Other head counts: the x3 GEMM."""
+    from . import _lib, x3
 
-    return x3.gemm(h, x3.pack(wh, prec="x3"), bias=bh)
+    M, K = h.shape
+    if wh.shape[0] != 6 or K % 4 or K > 1024:
+        return x3.gemm(h, x3.pack(wh, prec="x3"), bias=bh)
+    h, wh, bh = h.contiguous(), wh.contiguous(), bh.contiguous()
+    out = torch.empty((M, 6), dtype=torch.float32, device=h.device)
+    step = max(1, (2 ** 31 - 1) // (4 * K))  # rows per call: the kernel's buffer resource spans < 2^31 bytes
+    for r0 in range(0, M, step):
+        m = min(step, M - r0)
+        _lib.check(_lib.lib().mm_heads_fwd(_lib.ptr(h[r0:r0 + m]), K, K, _lib.ptr(wh), _lib.ptr(bh), m,
+                                            _lib.ptr(out[r0:r0 + m]), _lib.stream_ptr()), "mm_heads_fwd")
+    return out
 
 
 def _heads_bwd(dz, h, wh, bits, out_w=None, out_b=None):

@@ -197,3 +197,24 @@ def test_head_sample_matches_unfused_path():
     assert legal.all()
     jr = lp1.view(-1)[: M - 1:2] + lp1.view(-1)[1:M:2]
     torch.testing.assert_close(j1[: (M - 1) // 2 + 0][: jr.numel()], jr, rtol=0, atol=0, equal_nan=True)
+    # the update's heads forward (mm_heads_fwd) takes mm_head_sample's arithmetic: the same logits bit for bit,
+    # so the PPO ratio of a fresh batch is exactly 1 at the rollout's parameters
+    with torch.no_grad():
+        z = actor.logits(x)
+    assert torch.equal(z, logits)
+
+
+@pytest.mark.parametrize("K", [128, 264, 1024])
+def test_heads_fwd_vs_fp64(K):
+    """mm_heads_fwd at the unrolled width (264) and the runtime-loop widths, ragged row counts, against fp64."""
+    from marlmaze.networks import _heads_fwd
+
+    g = torch.Generator(device="cuda").manual_seed(K)
+    for M in (1, 31, 33, 5000):
+        h = torch.rand(M, K, device="cuda", generator=g) * 3
+        w = torch.randn(6, K, device="cuda", generator=g) * 0.05
+        b = torch.randn(6, device="cuda", generator=g)
+        z = _heads_fwd(h, w, b)
+        ref = h.double() @ w.double().T + b.double()
+        err = (z.double() - ref).abs().max().item()
+        assert err <= 1e-5 * ref.abs().max().item(), (K, M, err)
