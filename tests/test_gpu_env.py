@@ -191,11 +191,12 @@ def test_65536_mazes_10x10_match_oracle():
         masks = om
 
 
-def test_big_layouts_both_step_forms_match_oracle():
-    """The env-step kernel has a latency form (grid <= 2 workgroups per CU: every lane replays both agents,
-    and 20x20 layouts split each lane's two directions over the half-wavefronts) and a throughput form
-    (the replays handed between the wavefronts).  The random-play tests run small batches (latency form);
-    here 20x20 mazes above 2 x 256 CUs x 16 mazes per workgroup take the throughput form, with resets."""
+def test_big_layouts_many_workgroup_rounds_match_oracle():
+    """Large layouts (16 mazes per workgroup) step in the latency form (every lane replays both agents; each
+    lane's two directions split over the half-wavefronts) at every batch size; layouts up to 1 KB switch to
+    the throughput form (replays handed between the wavefronts) above 2 workgroups per CU, which the
+    65,536-maze 10x10 test runs.  Here 20x20 mazes above 2 x 256 CUs x 16 mazes per workgroup (several
+    workgroup rounds per CU), with resets."""
     n, steps = 9000, 40
     cfg = dict(default_size=(20, 20), max_timestep=30)
     seeds = np.arange(n, dtype=np.uint64) * np.uint64(31) + np.uint64(5)
