@@ -495,3 +495,24 @@ def test_graph_rollout_equals_eager(n):
         for k in outs[0]:
             assert torch.equal(outs[0][k], outs[1][k]), (it, k)
     assert ags[1]._graph is not None and ags[0]._sample_offset == ags[1]._sample_offset
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_fresh_batch_logp_matches_rollout(dtype):
+    """Before the first optimizer step, the update's log-probs of a fresh rollout batch equal the rollout's
+    (PPO ratio 1): the update's actor forward takes the same trunk kernels per row and its heads
+    (mm_heads_fwd) the rollout's fused-head arithmetic (mm_head_sample), for fp32-class and fp16 GEMMs alike;
+    only the log-softmax formula differs (torch's vs the sampler's), hence 1e-5."""
+    torch.manual_seed(5)
+    ag = _agent(n_envs=512, horizon=8, dtype=dtype, sample_seed=3,
+                env_config=dict(default_size=(10, 10), max_timestep=1200, seed_base=0))
+    with torch.no_grad():
+        ag.actor.move_head.weight.mul_(30.0)  # non-trivial policies (the 0.01 init makes every logit ~0)
+        ag.actor.mark_head.weight.mul_(30.0)
+    b_obs, b_act, b_lp, _, _, b_masks, _, _ = ag.get_batch()
+    with torch.no_grad():
+        lp = ag.policy_logp(b_obs, b_act, b_masks)
+    fin = torch.isfinite(b_lp)
+    assert fin.float().mean().item() > 0.99
+    err = (lp[fin] - b_lp[fin]).abs().max().item()
+    assert err <= 1e-5, (dtype, err)
