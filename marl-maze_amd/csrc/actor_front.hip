@@ -805,14 +805,14 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
 constexpr int kQp = 44;                      // QKV row pitch (floats): [32 tokens][44]
 constexpr int kQO = 0, kKO = 12, kVO = 24;   // q | 0 0 | k | 0 0 | v
-constexpr int kTp = 36;                      // transpose buffer T [j][i], pitch 36 (j-major)
+constexpr int kTp = 36;                      // transpose buffer T [i][j], pitch 36 (query-major, rows i < 24)
 // per sample: QKV [23][44], then T [23][36], then the reduction operands G [23][40] | x [23][4] (dctx is
 // read from dh).  The padding tokens' rows 23-31 of QKV and T are read past the rows written -- the next
 // words of the workgroup's LDS, zeroed at the start, finite ever after: every product keeps them out of
 // the results (S^T and dP^T rows / columns >= 23 are masked out of the softmax, P and dS are 0 there)
 constexpr int kMG = 0, kMX = kTok * kQkv;
 constexpr int kMSample = kMX + kTok * kPin;  // 1,012 floats per sample
-static_assert(kTok * kQp <= kMSample && kTok * kTp <= kMSample, "QKV and T live in the sample's region");
+static_assert(kTok * kQp <= kMSample && 24 * kTp <= kMSample, "QKV and T live in the sample's region");
 // zeroed words after the last sample's region, so that its padding rows read this kernel's own data (words
 // of another kernel could hold anything, and a huge finite value times the zero weight it gets is not 0)
 constexpr int kMPad = ((32 * kQp > 32 * kTp ? 32 * kQp : 32 * kTp) - kMSample + 3) & ~3;
@@ -1161,16 +1161,17 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             }
             f32x4_t (&P)[2][2] = S;
             f32x4_t (&dS)[2][2] = dP;
-            wave_sync();  // the QKV words are dead: the transpose buffer (rows j < 23)
+            wave_sync();  // the QKV words are dead: the transpose buffer
+            // T [i][j] (query-major, rows i < 24, pitch kTp): a C tile's four registers g are consecutive j, so a
+            // lane stores them as one 16-byte write (P and dS are 0 in the padding rows and columns)
             float* T = my;
-            // ---- dV = P^T dctx: rows j, columns c (20 -> 32); k = i = 16 ib + 4 q4 + e ----
+            // ---- dV = P^T dctx: rows j, columns c (20 -> 32); k = i = kh_row(s, q4) ----
 #pragma unroll
-            for (int J = 0; J < 2; J++)
+            for (int I = 0; I < 2; I++)
+                if (16 * I + c16 < 24)
 #pragma unroll
-                for (int I = 0; I < 2; I++)
-#pragma unroll
-                    for (int g = 0; g < 4; g++)
-                        if (16 * J + 4 * q4 + g < kTok) T[(16 * J + 4 * q4 + g) * kTp + 16 * I + c16] = P[J][I][g];
+                    for (int J = 0; J < 2; J++)
+                        *reinterpret_cast<f32x4_t*>(T + (16 * I + c16) * kTp + 16 * J + 4 * q4) = P[J][I];
             wave_sync();
             f32x4_t dV[2][2];
 #pragma unroll
@@ -1184,7 +1185,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 const int i = kh_row(s, q4);
                 float pa[2];
 #pragma unroll
-                for (int J = 0; J < 2; J++) pa[J] = T[(16 * J + c16) * kTp + i];
+                for (int J = 0; J < 2; J++) pa[J] = T[i * kTp + 16 * J + c16];
                 const float* dr = dhr + min(i, kTok - 1) * kEmb;
                 const float db[2] = {dr[c16], dr[min(16 + c16, kEmb - 1)]};
 #pragma unroll
@@ -1194,12 +1195,11 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             }
             wave_sync();  // P^T reads done: dS^T into the same buffer
 #pragma unroll
-            for (int J = 0; J < 2; J++)
+            for (int I = 0; I < 2; I++)
+                if (16 * I + c16 < 24)
 #pragma unroll
-                for (int I = 0; I < 2; I++)
-#pragma unroll
-                    for (int g = 0; g < 4; g++)
-                        if (16 * J + 4 * q4 + g < kTok) T[(16 * J + 4 * q4 + g) * kTp + 16 * I + c16] = dS[J][I][g];
+                    for (int J = 0; J < 2; J++)
+                        *reinterpret_cast<f32x4_t*>(T + (16 * I + c16) * kTp + 16 * J + 4 * q4) = dS[J][I];
             wave_sync();
             // ---- dK = dS^T Q: rows j, columns a (10 of 16); k = i = kh_row(s, q4) ----
             // ---- dQ^T = K^T dS^T: rows a = 4 q4 + g (10 of 16), columns i; k = j = kh_row(s, q4): B = dS^T rows
@@ -1210,9 +1210,10 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             for (int s = 0; s < kKH; s++) {
                 const int i = kh_row(s, q4);
 #pragma unroll
-                for (int J = 0; J < 2; J++) dK[J] = mfma4(T[(16 * J + c16) * kTp + i], qb[s], dK[J]);
+                for (int J = 0; J < 2; J++) dK[J] = mfma4(T[i * kTp + 16 * J + c16], qb[s], dK[J]);
 #pragma unroll
-                for (int I = 0; I < 2; I++) dQ[I] = mfma4(ka[s], T[i * kTp + 16 * I + c16], dQ[I]);
+                for (int I = 0; I < 2; I++)  // (query rows i >= 24 hold other words: their dQ columns are not kept)
+                    dQ[I] = mfma4(ka[s], T[(16 * I + c16) * kTp + i], dQ[I]);
             }
             wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
 #pragma unroll
