@@ -331,42 +331,43 @@ class PPO:
         last_end = torch.full((n,), -1, dtype=torch.int64, device=dev)
         t0, t_stop, end_at_stop = 0, None, None
         t_min = limit // n  # the first step after which the batch can be full
-        while t_stop is None:
-            C = min(self.episode_chunk, t_min - t0) if t0 < t_min else 1
-            ch = dict(obs=torch.empty((C + 1, n, 2, 65), dtype=torch.float32, device=dev),
-                      masks=torch.empty((C + 1, n, 2, 6), dtype=torch.uint8, device=dev),
-                      act=torch.empty((C, n, 2, 2), dtype=torch.int8, device=dev),
-                      logp=torch.empty((C, n), dtype=torch.float32, device=dev),
-                      rowlogp=torch.empty((C, 2 * n), dtype=torch.float32, device=dev),
-                      val=torch.empty((C, n), dtype=torch.float32, device=dev),
-                      rew=torch.empty((C, n), dtype=torch.float32, device=dev),
-                      done=torch.empty((C, n), dtype=torch.uint8, device=dev),
-                      stats=torch.empty((C, n, 2), dtype=torch.int32, device=dev))
-            ch["obs"][0].copy_(obs0)
-            ch["masks"][0].copy_(masks0)
-            for t in range(C):
-                ch["val"][t] = self.critic(ch["obs"][t]).view(n)
-                h = self.actor.trunk(ch["obs"][t].view(2 * n, 65))
-                ops.head_sample(h, head_w, head_b, ch["masks"][t].view(2 * n, 6), self.sample_seed,
-                                self._sample_offset, actions=ch["act"][t].view(2 * n, 2), logp=ch["rowlogp"][t],
-                                joint_logp=ch["logp"][t])
-                self._sample_offset += 1
-                self.venv.step(ch["act"][t], auto_reset=True, obs=ch["obs"][t + 1], masks=ch["masks"][t + 1],
-                               reward=ch["rew"][t], done=ch["done"][t], ep_stats=ch["stats"][t])
-            chunks.append(ch)
-            obs0, masks0 = ch["obs"][C], ch["masks"][C]
-            # completed-episode steps after each step of the chunk: sum over mazes of (last end + 1)
-            tt = torch.arange(t0, t0 + C, device=dev).view(C, 1)
-            ends = torch.where(ch["done"].bool(), tt, torch.full_like(tt, -1))
-            ends = torch.maximum(torch.cummax(ends, 0).values, last_end.view(1, n))
-            filled = (ends + 1).sum(1)
-            hit = torch.nonzero(filled > limit)
-            if hit.numel():  # one host synchronisation per chunk; only the last chunk can hit (at its end)
-                k = int(hit[0, 0])
-                t_stop, end_at_stop = t0 + k, ends[k]
-            else:
-                last_end = ends[-1]
-                t0 += C
+        with x3.cached_packs():  # the weights are fixed during the batch: packed once, not per step
+            while t_stop is None:
+                C = min(self.episode_chunk, t_min - t0) if t0 < t_min else 1
+                ch = dict(obs=torch.empty((C + 1, n, 2, 65), dtype=torch.float32, device=dev),
+                          masks=torch.empty((C + 1, n, 2, 6), dtype=torch.uint8, device=dev),
+                          act=torch.empty((C, n, 2, 2), dtype=torch.int8, device=dev),
+                          logp=torch.empty((C, n), dtype=torch.float32, device=dev),
+                          rowlogp=torch.empty((C, 2 * n), dtype=torch.float32, device=dev),
+                          val=torch.empty((C, n), dtype=torch.float32, device=dev),
+                          rew=torch.empty((C, n), dtype=torch.float32, device=dev),
+                          done=torch.empty((C, n), dtype=torch.uint8, device=dev),
+                          stats=torch.empty((C, n, 2), dtype=torch.int32, device=dev))
+                ch["obs"][0].copy_(obs0)
+                ch["masks"][0].copy_(masks0)
+                for t in range(C):
+                    ch["val"][t] = self.critic(ch["obs"][t]).view(n)
+                    h = self.actor.trunk(ch["obs"][t].view(2 * n, 65))
+                    ops.head_sample(h, head_w, head_b, ch["masks"][t].view(2 * n, 6), self.sample_seed,
+                                    self._sample_offset, actions=ch["act"][t].view(2 * n, 2), logp=ch["rowlogp"][t],
+                                    joint_logp=ch["logp"][t])
+                    self._sample_offset += 1
+                    self.venv.step(ch["act"][t], auto_reset=True, obs=ch["obs"][t + 1], masks=ch["masks"][t + 1],
+                                   reward=ch["rew"][t], done=ch["done"][t], ep_stats=ch["stats"][t])
+                chunks.append(ch)
+                obs0, masks0 = ch["obs"][C], ch["masks"][C]
+                # completed-episode steps after each step of the chunk: sum over mazes of (last end + 1)
+                tt = torch.arange(t0, t0 + C, device=dev).view(C, 1)
+                ends = torch.where(ch["done"].bool(), tt, torch.full_like(tt, -1))
+                ends = torch.maximum(torch.cummax(ends, 0).values, last_end.view(1, n))
+                filled = (ends + 1).sum(1)
+                hit = torch.nonzero(filled > limit)
+                if hit.numel():  # one host synchronisation per chunk; only the last chunk can hit (at its end)
+                    k = int(hit[0, 0])
+                    t_stop, end_at_stop = t0 + k, ends[k]
+                else:
+                    last_end = ends[-1]
+                    t0 += C
         Ts = t_stop + 1  # == the steps taken (the last chunk ends at t_stop)
         cat = {k: torch.cat([c[k][:c["act"].shape[0]] for c in chunks], 0)[:Ts]
                for k in ("obs", "masks", "act", "logp", "val", "rew", "done", "stats")}
