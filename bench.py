@@ -16,6 +16,7 @@ Launch: python bench.py [--gpus 1 --steps K --warmup W]
         python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -134,6 +135,24 @@ def cpu_baseline():
                 runs=runs)
 
 
+def _workload_label(n, size, dtype):
+    """The BASELINE.json config a run measures (the label names what actually ran)."""
+    loop = "PPO rollout+GAE+update"
+    if dtype == "f16":
+        share = (" (configs[4]: 262,144 mazes over 8 GPUs, fp16 actor/critic)" if size == 10 and n * 8 == 262144
+                 else " (fp16 actor/critic)")
+        return f"{loop} over {n} parallel {size}x{size} 2-agent mazes per GPU, fp16 GEMMs{share}"
+    if size == 10 and n == 65536:
+        tag = "configs[2], the north-star workload: 65,536 parallel 10x10 mazes per GPU"
+    elif size == 10 and n == 4096:
+        tag = "configs[1]: 4,096 parallel 10x10 mazes"
+    elif size == 20 and n * 8 == 65536:
+        tag = "configs[3] per-GPU share: 65,536 20x20 mazes over 8 GPUs = 8,192 per GPU"
+    else:
+        tag = "not a BASELINE config"
+    return f"{loop} over {n} parallel {size}x{size} 2-agent mazes per GPU ({tag})"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,11 +244,14 @@ def main():
     minibatches_per_iter = agent.updates_per_batch * len(range(0, batch_global // world, (batch_global // world) // 5))
     total_steps = world * n * T * a.steps
 
-    traffic = None
-    pmc = os.path.join(REPO, "profiles", f"pmc_env_step_{n}x{a.size}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
+    # HBM traffic of k_step from the latest round's PMC file for this workload (tools/pmc_bench.sh:
+    # FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 x2 FETCH correction), per launch
+    traffic, traffic_src = None, None
+    pmcs = sorted(glob.glob(os.path.join(REPO, "profiles", f"r[0-9][0-9]_pmc_env_step_{n}x{a.size}.json")))
+    if pmcs:
+        with open(pmcs[-1]) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+        traffic_src = os.path.relpath(pmcs[-1], REPO)
 
     line = {
         "metric": "env-steps/sec (2-agent 10x10 maze) + PPO updates/sec",
@@ -246,10 +268,7 @@ def main():
         "data": "synthetic: procedurally generated mazes (CPython-MT seeds 0..N-1 per GPU), random-init "
                 "actor/critic (torch.manual_seed(3234)), actions sampled by the policy",
         "config": {
-            "workload": (f"PPO rollout+GAE+update over {n} parallel {a.size}x{a.size} 2-agent mazes per GPU "
-                         f"(configs[1] loop at configs[2] scale)") if a.dtype == "f32" else
-                        (f"PPO rollout+GAE+update over {n} parallel {a.size}x{a.size} 2-agent mazes per GPU, fp16 "
-                         f"actor/critic GEMMs, 6 logits (configs[4]: 262,144 mazes at 8 GPUs)"),
+            "workload": _workload_label(n, a.size, a.dtype),
             "mazes_per_gpu": n, "maze": f"{a.size}x{a.size} (layout {H}x{H})", "max_timestep": a.max_t,
             "horizon": T, "global_batch": batch_global, "minibatch": batch_global // 5,
             "minibatch_steps_per_iter": minibatches_per_iter, "parallelism": f"dp{world}",
@@ -261,7 +280,7 @@ def main():
         "rollout_env_steps_per_sec": total_steps / (elapsed - sum(upd_ms) * 1e-3),
         "roofline": {
             "kernel": "k_step (mm_env_step)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
             "alg_bytes_per_env_step": alg_bytes, "launch_us": env_step_ms * 1e3, "launches": len(step_ms),
             "timed_in": "the timed region" if not graph else "one instrumented rollout after the timed region",
         },

@@ -232,7 +232,9 @@ class PPO:
     def _rollout_graph(self, b, n, T):
         """The rollout as a replay of a captured HIP graph (same kernels, same
         draws: the sampler reads its Philox base offset from the device)."""
-        key = (id(self.venv), self.flat.data.data_ptr() if self.flat is not None else None, T, id(b["obs"]))
+        # everything the captured launches hold by value: a change re-captures
+        key = (id(self.venv), self.flat.data.data_ptr() if self.flat is not None else None, T, id(b["obs"]),
+               self.sample_seed, float(self.discount_rate), float(self.lam), bool(self.bootstrap))
         if self._graph is None or self._graph_key != key:
             if not self._graph_warm:  # the first rollout runs uncaptured (one-time host work: kernel attributes)
                 self._graph_warm = True
@@ -309,12 +311,18 @@ class PPO:
         dropped (the reference keeps only complete episodes).  Samples are
         ordered maze by maze, each maze's episodes in time order (one maze: the
         reference's order), and GAE runs on whole episodes (PPO.py:133; the
-        episode-parallel walk of mm_gae_ex, bit-exact).  No step runs past t*
-        (a maze finishing there would draw its next maze from its RNG stream,
-        which the reference never does): after step t at most n (t + 1) steps
-        can belong to completed episodes, so steps before t = batch_size // n
-        run in chunks of ``episode_chunk`` with one host synchronisation per
-        chunk, later ones one at a time.
+        episode-parallel walk of mm_gae_ex, bit-exact).  No step past t* may
+        leave a trace (a maze finishing there would draw its next maze from its
+        RNG stream, which the reference never does): after step t at most n (t + 1) steps
+        can belong to completed episodes, so the steps before
+        t_min = batch_size // n run in chunks of ``episode_chunk`` with one host
+        synchronisation per chunk.  From t_min on the chunks grow geometrically
+        (1, 2, 4, ... up to ``episode_chunk`` steps) from an environment
+        snapshot: when the stop step falls inside a chunk, the environment is
+        rewound to the chunk's start and only the steps up to t* are replayed
+        with the recorded actions, so neither the MT19937 streams nor the
+        sampler's Philox offset carry any trace of the overshoot into the next
+        batch.
         """
         self._ensure_env()
         n, dev = self.n_envs, self.device
@@ -331,9 +339,15 @@ class PPO:
         last_end = torch.full((n,), -1, dtype=torch.int64, device=dev)
         t0, t_stop, end_at_stop = 0, None, None
         t_min = limit // n  # the first step after which the batch can be full
+        tail = 1  # the next chunk length past t_min
+        self._episode_replayed = 0
         with x3.cached_packs():  # the weights are fixed during the batch: packed once, not per step
             while t_stop is None:
-                C = min(self.episode_chunk, t_min - t0) if t0 < t_min else 1
+                if t0 < t_min:
+                    C, snap = min(self.episode_chunk, t_min - t0), None
+                else:
+                    C, tail = tail, min(2 * tail, self.episode_chunk)
+                    snap, off0 = self.venv.snapshot(), self._sample_offset
                 ch = dict(obs=torch.empty((C + 1, n, 2, 65), dtype=torch.float32, device=dev),
                           masks=torch.empty((C + 1, n, 2, 6), dtype=torch.uint8, device=dev),
                           act=torch.empty((C, n, 2, 2), dtype=torch.int8, device=dev),
@@ -362,13 +376,21 @@ class PPO:
                 ends = torch.maximum(torch.cummax(ends, 0).values, last_end.view(1, n))
                 filled = (ends + 1).sum(1)
                 hit = torch.nonzero(filled > limit)
-                if hit.numel():  # one host synchronisation per chunk; only the last chunk can hit (at its end)
+                if hit.numel():  # one host synchronisation per chunk; only a tail chunk can hit
                     k = int(hit[0, 0])
                     t_stop, end_at_stop = t0 + k, ends[k]
+                    if k + 1 < C:  # overshoot: rewind to the chunk's start, replay steps t0 .. t* only
+                        self.venv.restore(snap)
+                        for t in range(k + 1):
+                            self.venv.step(ch["act"][t], auto_reset=True, obs=ch["obs"][t + 1],
+                                           masks=ch["masks"][t + 1], reward=ch["rew"][t], done=ch["done"][t],
+                                           ep_stats=ch["stats"][t])
+                        self._sample_offset = off0 + k + 1
+                        self._episode_replayed = k + 1
                 else:
                     last_end = ends[-1]
                     t0 += C
-        Ts = t_stop + 1  # == the steps taken (the last chunk ends at t_stop)
+        Ts = t_stop + 1  # == the steps kept (the last chunk may hold discarded steps past t_stop)
         cat = {k: torch.cat([c[k][:c["act"].shape[0]] for c in chunks], 0)[:Ts]
                for k in ("obs", "masks", "act", "logp", "val", "rew", "done", "stats")}
         adv, rtg = ops.gae(cat["rew"], cat["val"], cat["done"], gamma=self.discount_rate, lam=self.lam)

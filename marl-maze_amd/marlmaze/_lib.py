@@ -107,6 +107,14 @@ def lib():
                 f"libmarlmaze.so not found at {LIB_PATH}: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
                 "There is no CPU fallback.")
+        if not os.environ.get("MARLMAZE_LIB"):  # the in-tree build must be of the sources in this tree
+            from . import _build
+
+            if _build.stored_hash() != _build.source_hash():
+                raise MMError(
+                    f"{LIB_PATH} was not built from the sources in this tree (its {os.path.basename(_build.HASH_FILE)} "
+                    "is missing or differs from the sha256 of csrc/ + include/): rebuild it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         P, i32, u64, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_float
         L.mm_version.restype = i32

@@ -369,7 +369,15 @@ class _EngineCritic(torch.autograd.Function):
 
 
 def _grad_of(p):
-    """p.grad, allocated if absent (the update writes every element)."""
+    """p.grad, allocated if absent (the update writes every element).  A parameter of a
+    marlmaze.update.FlatParams gets its view of the flat gradient buffer back if anything replaced or
+    cleared its .grad (nn.Module.zero_grad() sets it to None): the all-reduce and mm_clip_adam read the
+    flat buffer, so a gradient written anywhere else would be silently lost."""
+    flat = getattr(p, "_mm_flat_grad", None)
+    if flat is not None:
+        if p.grad is None or p.grad.data_ptr() != flat.data_ptr():
+            p.grad = flat
+        return p.grad
     if p.grad is None:
         p.grad = torch.empty_like(p)
     return p.grad

@@ -61,6 +61,7 @@ class FlatParams:
                 v.copy_(p.data)
                 p.data = v
                 p.grad = self.grad[o:o + p.numel()].view_as(p)
+                p._mm_flat_grad = p.grad  # networks._grad_of re-binds .grad to it if anything replaced it
 
     def seg_view(self, buf, k):
         o, n = self.segs[k]
@@ -141,8 +142,8 @@ class FlatAdam:
 
     # ---- the kernel's view ----
     def segment(self, max_norm, grad_scale=1.0):
-        """The mm_adam_seg_t of the NEXT step (advances the step counter)."""
-        self.t += 1
+        """The mm_adam_seg_t of the NEXT step, t + 1 (the caller advances ``t`` once the step is queued)."""
+        t = self.t + 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
         lr = float(g["lr"])
@@ -155,8 +156,8 @@ class FlatAdam:
         s.exp_avg_sq = self.exp_avg_sq.data_ptr() + 4 * o
         s.n = n
         s.max_norm = float(max_norm)
-        s.step_size = lr / (1.0 - b1 ** self.t)  # as the single-tensor Adam forms them (python floats)
-        s.bc2_sqrt = math.sqrt(1.0 - b2 ** self.t)
+        s.step_size = lr / (1.0 - b1 ** t)  # as the single-tensor Adam forms them (python floats)
+        s.bc2_sqrt = math.sqrt(1.0 - b2 ** t)
         s.grad_scale = float(grad_scale)
         return s
 
@@ -164,7 +165,13 @@ class FlatAdam:
 def clip_adam(opts, max_norm, norms=None, grad_scale=1.0):
     """clip_grad_norm_(params of each optimizer, max_norm) + each optimizer's Adam step in two launches
     (mm_clip_adam).  norms: optional f32 [len(opts)] device tensor receiving the unclipped norms.
-    grad_scale multiplies the gradients first (1 / world under data parallelism: the all-reduce sums)."""
+    grad_scale multiplies the gradients first (1 / world under data parallelism: the all-reduce sums).
+
+    Where this differs from clip_grad_norm_ + Adam.step (PPO.py:74-85), none of which the update reads:
+    the clipped (and, under DP, averaged) gradient lives only inside the kernel, so ``.grad`` keeps the
+    gradient as the backward (and the all-reduce: a SUM over ranks) left it; max_norm <= 0 means no
+    clipping (torch would scale every gradient to ~0; the reference always clips at 0.5).  The step
+    counters advance only once the launch is queued without error."""
     L = _lib.lib()
     f = opts[0].flat
     g0 = opts[0].param_groups[0]
@@ -177,6 +184,8 @@ def clip_adam(opts, max_norm, norms=None, grad_scale=1.0):
     b1, b2 = g0["betas"]
     _lib.check(L.mm_clip_adam(segs, len(opts), float(b1), float(b2), float(g0["eps"]), _lib.ptr(ws),
                               _lib.ptr(norms), _lib.stream_ptr()), "mm_clip_adam")
+    for o in opts:
+        o.t += 1
     x3.invalidate_packs()  # parameters changed behind torch's version counters
 
 

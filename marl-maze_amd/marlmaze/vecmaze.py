@@ -188,6 +188,25 @@ class VecMaze:
         self._kick_pregen()
         return obs, masks
 
+    def _state(self):
+        ts = [self.layout, self.agents, self.mazes, self.rng, self.work]
+        if self.pregen:
+            ts += [self.next_layout, self.next_mazes, self.next_rng, self.gen_state]
+        return ts
+
+    def snapshot(self):
+        """Device copies of every state buffer (the mazes, agents, MT19937 streams, the pre-generated next
+        mazes): restore() rewinds the environment to this point, stream-ordered, no host sync."""
+        self._quiesce_pregen()  # no generation in flight: the copies are one consistent state
+        return [t.clone() for t in self._state()]
+
+    def restore(self, snap):
+        """Rewind to a snapshot() (the steps since then, their resets and RNG draws are undone)."""
+        self._quiesce_pregen()  # generation queued since the snapshot must not land after the rewind
+        for t, s in zip(self._state(), snap):
+            t.copy_(s)
+        self._kick_pregen()  # mazes whose next maze was pending at the snapshot
+
     # ------------------------------------------------------------------
     # host-side introspection (tests, facades, stats) -- synchronising
     # ------------------------------------------------------------------

@@ -199,10 +199,11 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None):
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dy.stride(1) == 1 and x.stride(1) == 1
+    defer = bool(_DEFER) and out is not None and M > 0  # a result the caller reads now is never deferred
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
     L = _lib.lib()
-    if _DEFER and M > 0:
+    if defer:
         assert out.is_contiguous()
         S = L.mm_gemm_wgrad_slices(PRECS[prec], M, N, K)
         _lib.check(S if S < 0 else 0, "mm_gemm_wgrad_slices")
@@ -268,11 +269,12 @@ def colsum(x, out=None, slabs=256):
     ``out`` given (and the default slabs), the sum runs when the scope ends."""
     x = x.contiguous()
     R, N = x.shape
+    defer = bool(_DEFER) and out is not None and slabs == 256  # a result the caller reads now is never deferred
     if out is None:
         out = torch.empty(N, dtype=torch.float32, device=x.device)
     if R == 0:
         return out.zero_()
-    if _DEFER and slabs == 256:
+    if defer:
         assert out.is_contiguous() and out.numel() == N
         d = _DEFER[-1]
         d.cols.append(_lib.ColsumSeg(_lib.ptr(x), int(R), int(N), _lib.ptr(out)))

@@ -11,6 +11,8 @@ the reference GAE per whole episode on the same values, returns (adv + V)
 within 1e-5 (atol 1e-5) of the oracle's own, and two batches in a row (each
 batch starts from a fresh maze, PPO.py:104, so the RNG streams must agree).
 """
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -39,16 +41,27 @@ def _segments(done_row, upto):
     return out
 
 
-@pytest.mark.parametrize("n,bs", [(1, 400), (48, 1500)])
-def test_episode_batches_match_reference(n, bs):
-    cfg = dict(default_size=(6, 6), max_timestep=30)
-    ag = _agent(n_envs=n, batch_size=bs, episode_batches=True, episode_chunk=8, sample_seed=11,
-                env_config=dict(cfg, seed_base=70))
+# (mazes, batch_size, side, max_timestep, episode_chunk); the last case is BASELINE configs[0] -- the reference's
+# own run, main.py:17-20 at 10x10: PPO(agent_amount=2, batch_size=15000, lr=0.00014) on ONE maze, max_timestep
+# 1200 -- through the drop-in: ~15,000 single-maze steps per batch, two batches in a row
+CASES = [(1, 400, 6, 30, 8), (48, 1500, 6, 30, 8), (1, 15000, 10, 1200, 64)]
+
+
+@pytest.mark.parametrize("n,bs,side,max_t,chunk", CASES, ids=["1maze", "48mazes", "configs0"])
+def test_episode_batches_match_reference(n, bs, side, max_t, chunk):
+    cfg = dict(default_size=(side, side), max_timestep=max_t)
+    ag = _agent(n_envs=n, batch_size=bs, episode_batches=True, episode_chunk=chunk, sample_seed=11,
+                env_config=dict(cfg, seed_base=70), lr=0.00014)
     ora = OracleEnv(n, seeds=np.arange(n, dtype=np.uint64) + np.uint64(70), **cfg)
     oc = oppo.OCritic()
     oc.load_state_dict({k: v.detach().cpu() for k, v in ag.critic.state_dict().items()})
     for batch in range(2):
+        torch.cuda.synchronize()
+        t_start = time.time()
         b_obs, b_act, b_lp, b_sp, ep_lens, b_masks, b_adv, b_val = ag.get_batch()
+        torch.cuda.synchronize()
+        print(f"get_batch {batch}: {time.time() - t_start:.2f} s for {ag._episode_info['t_stop'] + 1} steps x {n} "
+              f"mazes ({b_obs.shape[0]} samples kept, {ag._episode_replayed} replayed after the rewind)")
         info = ag._episode_info
         A = info["act"].cpu().numpy()
         Ts = info["t_stop"] + 1
@@ -112,3 +125,40 @@ def test_episode_batches_train_epoch():
     assert len(ag.history) == 2
     for h in ag.history:
         assert h["episodes"] > 0 and np.isfinite([h["actor_loss"], h["critic_loss"]]).all()
+
+
+def test_snapshot_restore_rewinds_every_stream():
+    """VecMaze.snapshot / restore (the episode batch's rewind): the steps after a
+    restore, with the same actions, repeat the first pass bit for bit, resets and
+    MT19937 draws included, and the state after them is the same."""
+    from marlmaze.vecmaze import VecMaze
+
+    n, steps = 64, 60
+    env = VecMaze(n, default_size=(5, 5), max_timestep=20, seeds=np.arange(n, dtype=np.uint64) + np.uint64(5))
+    obs, masks = env.reset()
+    rng = np.random.default_rng(1)
+    for _ in range(7):  # somewhere mid-episode
+        m = masks.cpu().numpy().astype(bool)
+        mv = np.where(m[..., :5].any(-1), np.argmax(rng.random(m[..., :5].shape) * m[..., :5], -1), 4)
+        obs, masks, _, _ = env.step(torch.as_tensor(np.stack([mv, np.zeros_like(mv)], -1).astype(np.int8)).cuda())
+    snap = env.snapshot()
+    acts, first = [], []
+    for _ in range(steps):
+        m = masks.cpu().numpy().astype(bool)
+        mv = np.where(m[..., :5].any(-1), np.argmax(rng.random(m[..., :5].shape) * m[..., :5], -1), 4)
+        mk = (rng.random((n, 2)) < 0.5) & m[..., 5]
+        a = torch.as_tensor(np.stack([mv, mk], -1).astype(np.int8)).cuda()
+        acts.append(a)
+        obs, masks, r, d = env.step(a)
+        first.append((obs.clone(), masks.clone(), r.clone(), d.clone()))
+    assert sum(int(f[3].sum()) for f in first) > n  # many resets (and MT draws) in the window
+    after = [t.clone() for t in env._state()]
+    env.restore(snap)
+    for t, s in zip(env._state(), snap):
+        assert torch.equal(t, s)
+    for a, (o1, m1, r1, d1) in zip(acts, first):
+        obs, masks, r, d = env.step(a)
+        assert torch.equal(obs, o1) and torch.equal(masks, m1) and torch.equal(r, r1) and torch.equal(d, d1)
+    # mazes, agents, MT streams, done list (the pre-generation buffers' progress is asynchronous)
+    for t, s in zip(env._state()[:5], after[:5]):
+        assert torch.equal(t, s)

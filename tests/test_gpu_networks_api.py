@@ -1,0 +1,83 @@
+"""The explicit backward used outside PPO's flat buffers (Actor / Critic as
+stand-alone modules, networks.py:13-106) and .grad handling around it.
+
+* A stand-alone Actor's heads are separate tensors (not the back-to-back pair
+  update.FlatParams lays out), so train_backward copies the heads' gradients
+  into their own .grad.  Inside an x3.deferred() scope that copy must read a
+  finished result: the gradients must equal, bit for bit, those of the same
+  backward outside the scope.
+* nn.Module.zero_grad() (set_to_none=True) drops the .grad views of PPO's flat
+  gradient buffer.  The explicit backward re-binds them, so the all-reduce and
+  mm_clip_adam, which read the flat buffer, still see every gradient.
+"""
+import numpy as np
+import pytest
+import torch
+
+from marlmaze import x3
+from marlmaze.PPO import PPO
+from marlmaze.networks import Actor
+from oracle import ppo as oppo
+
+pytestmark = pytest.mark.gpu
+
+
+def _actor_from_fixture(fx):
+    a = Actor([264, 264, 264]).cuda()
+    a.load_state_dict({k[6:]: torch.as_tensor(fx[k]).cuda() for k in fx.files if k.startswith("actor/")})
+    return a
+
+
+def _grads(mod):
+    return {k: p.grad.detach().clone() for k, p in mod.named_parameters()}
+
+
+@pytest.mark.parametrize("rows", [512, 20000])
+def test_standalone_actor_backward_inside_deferred(golden, rows):
+    fx = golden("nets")
+    actor = _actor_from_fixture(fx)
+    obs = torch.as_tensor(fx["obs"]).reshape(-1, 65)
+    x = obs[torch.arange(rows) % obs.shape[0]].cuda().contiguous()
+    g = torch.Generator().manual_seed(rows)
+    dz = (torch.randn((rows, 6), generator=g) / rows).cuda()
+    z, saved = actor.train_forward(x)
+    actor.train_backward(saved, dz)
+    ref = _grads(actor)
+    actor.zero_grad(set_to_none=True)
+    z2, saved2 = actor.train_forward(x)
+    with x3.deferred():
+        actor.train_backward(saved2, dz)
+    got = _grads(actor)
+    assert torch.equal(z, z2)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
+    # and the gradients are the autograd ones of the same actor (loose: summation order differs)
+    a64 = oppo.OActor()
+    a64.load_state_dict({k[6:]: torch.as_tensor(fx[k]) for k in fx.files if k.startswith("actor/")})
+    a64 = a64.double()
+    ml, kl = a64(x.cpu().double())
+    (torch.cat([ml, kl], 1) * dz.cpu().double()).sum().backward()
+    for k, p in a64.named_parameters():
+        r = p.grad.double()
+        cos = torch.nn.functional.cosine_similarity(got[k].cpu().double().flatten(), r.flatten(), 0).item()
+        assert cos > 0.9999 or r.abs().max().item() == 0, (k, cos)
+
+
+def test_zero_grad_set_to_none_rebinds_flat_buffer(golden):
+    fx = golden("nets")
+    ag = PPO(2, load=False, verbose=False, save=False, lr=0.00014, n_envs=16)
+    ag.actor.load_state_dict({k[6:]: torch.as_tensor(fx[k]).cuda() for k in fx.files if k.startswith("actor/")})
+    ag.critic.load_state_dict({k[7:]: torch.as_tensor(fx[k]).cuda() for k in fx.files if k.startswith("critic/")})
+    batch = tuple(torch.as_tensor(fx[k]).cuda() for k in ("obs", "actions", "old_logp", "advs", "rtgs", "masks"))
+    ag.minibatch_grads(*batch)
+    ref = ag.flat.grad.clone()
+    ag.flat.grad.fill_(float("nan"))
+    ag.actor.zero_grad()  # set_to_none=True: the .grad views are gone
+    ag.critic.zero_grad()
+    assert all(p.grad is None for p in ag.actor.parameters())
+    ag.minibatch_grads(*batch)
+    assert torch.equal(ag.flat.grad, ref)
+    lo, hi = ag.flat.grad.data_ptr(), ag.flat.grad.data_ptr() + 4 * ag.flat.numel
+    for p in list(ag.actor.parameters()) + list(ag.critic.parameters()):
+        assert lo <= p.grad.data_ptr() < hi
+    assert np.isfinite(ref.cpu().numpy()).all()
