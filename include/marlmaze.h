@@ -256,8 +256,14 @@ int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits
  * (dY) operand before its fp16 rounding and cscale the result (powers of two:
  * exact; a gradient far below 1 keeps fp16 precision).  X3 requires 1.0 for
  * all scales.
+ * MM_PREC_X2: fp32-class on two fp16 planes per operand: (x s) = hi + 2^-11 lo,
+ * hi = RN16(x s), lo = RN16(2^11 (x s - hi)) -- 22 significand bits for
+ * 2^-14 <= |x s| <= 2^15 (the 2^11 keeps lo out of the fp16 subnormals), three
+ * f16 MFMAs per product (hi hi into one accumulator; hi lo + lo hi into a
+ * second, added with weight 2^-11 before the epilogue) instead of X3's six
+ * bf16 ones, and two B planes instead of three.  Scales as for F16.
  * mm_gemm_tp_len / mm_gemm_tp_pack: the TP form of B for that precision (P_F16:
- * one 1-KiB plane per block).
+ * one 1-KiB plane per block; P_X2: two).
  * mm_gemm_nt: c = cscale (ascale A . B^T) (+ bias)(ReLU) -- mm_x3_nt_f32a's
  * forward (mbits_out) and input-gradient (mbits_in, colsum) forms; A fp32
  * [M, lda] with K, lda % 4 == 0 and 16-byte alignment, or (outputs N <= 64,
@@ -268,6 +274,7 @@ int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits
  * [mm_gemm_wgrad_ws_len(M, N, K)] floats, summed in a fixed order. */
 #define MM_PREC_X3 0
 #define MM_PREC_F16 1
+#define MM_PREC_X2 2
 long mm_gemm_tp_len(int prec, int R, int C);
 int mm_gemm_tp_pack(int prec, const float* X, int R, int C, int ld, int trans, uint16_t* tp, void* stream);
 int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
@@ -430,7 +437,8 @@ int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, int B, int p
 /* Backward of mm_actor_front_fwd for the upstream gradient dh [B, 460]: a
  * persistent grid of `grid` workgroups (2 per CU is the design point), each
  * writing one row of partial [grid, mm_actor_front_partial_len()]; the rows
- * are then summed into red [mm_actor_front_partial_len()] and turned into
+ * are then summed in fp64 into red (8-byte aligned, room for
+ * 2 x mm_actor_front_partial_len() floats = that many doubles) and turned into
  * grad [mm_actor_front_grad_len()] = [dwq 10x20 | dwk 10x20 | dwv 20x20 |
  * dwp 23x20x4 (embedding i's weight gradient zero-padded to 4 inputs) |
  * dbp 23x20].  Every sum has a fixed order (deterministic). */

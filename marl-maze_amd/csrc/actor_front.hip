@@ -1251,21 +1251,24 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
 
 // sum of the partial rows: workgroup = 64 columns x 16 row classes (r mod 16);
 // each thread sums its class in row order, then the 16 class sums are added in
-// class order (fixed order: deterministic)
+// class order (fixed order: deterministic).  In fp64: the parameter gradients
+// are differences of these sums (dbp_i = f_i + Wqkv^T e_i nearly cancels under
+// quirk Q1, where every row of a feature sees the same few inputs), so their
+// rounding must stay far below the gradients' own size.
 constexpr int kSumCols = 64, kSumClasses = 16;
 
 __global__ __launch_bounds__(kSumCols * kSumClasses) void k_front_sum(const float* __restrict__ partial, int rows,
-                                                                      float* __restrict__ red) {
-    __shared__ float acc_s[kSumClasses][kSumCols];
+                                                                      double* __restrict__ red) {
+    __shared__ double acc_s[kSumClasses][kSumCols];
     const int c = threadIdx.x % kSumCols, k = threadIdx.x / kSumCols;
     const int e = blockIdx.x * kSumCols + c;
-    float acc = 0.f;
+    double acc = 0.0;
     if (e < kPartLen)
-        for (int r = k; r < rows; r += kSumClasses) acc += partial[(size_t)r * kPartLen + e];
+        for (int r = k; r < rows; r += kSumClasses) acc += (double)partial[(size_t)r * kPartLen + e];
     acc_s[k][c] = acc;
     __syncthreads();
     if (k == 0 && e < kPartLen) {
-        float t = 0.f;
+        double t = 0.0;
 #pragma unroll
         for (int q = 0; q < kSumClasses; q++) t += acc_s[q][c];
         red[e] = t;
@@ -1286,11 +1289,12 @@ struct FrontGradPtrs {
 
 // SCATTER = false: the packed layout grad [kGradLen]; true: the per-parameter destinations dst
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_front_combine(const float* __restrict__ ws, const float* __restrict__ red,
+__global__ __launch_bounds__(256) void k_front_combine(const float* __restrict__ ws, const double* __restrict__ red,
                                                        float* __restrict__ grad, FrontGradPtrs dst) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= kGradLen) return;
-    auto put = [&](float v) {
+    auto put = [&](double vd) {
+        const float v = (float)vd;
         if (!SCATTER) {
             grad[e] = v;
         } else if (e < kGP) {
@@ -1308,24 +1312,24 @@ __global__ __launch_bounds__(256) void k_front_combine(const float* __restrict__
     const float* W = ws + kWsW;  // [40][20]
     if (e < kGP) {
         const int r = e / kEmb, c = e % kEmb;
-        float acc = 0.f;
+        double acc = 0.0;
         for (int tk = 0; tk < kTok; tk++) {
             const float* Wp = ws + kWsWP + (tk * kEmb + c) * kPin;  // Wp_i[c][0..3] (zero beyond d_i)
-            const float* E = red + kPEF + (tk * kGd + r) * kPin;    // E_i[r][0..3]
+            const double* E = red + kPEF + (tk * kGd + r) * kPin;   // E_i[r][0..3]
 #pragma unroll
-            for (int a = 0; a < kPin; a++) acc = fmaf(E[a], Wp[a], acc);
-            acc = fmaf(red[kPef + tk * kGd + r], ws[kWsBP + tk * kEmb + c], acc);  // e_i[r] b_i[c]
+            for (int a = 0; a < kPin; a++) acc = fma(E[a], (double)Wp[a], acc);
+            acc = fma(red[kPef + tk * kGd + r], (double)ws[kWsBP + tk * kEmb + c], acc);  // e_i[r] b_i[c]
         }
         put(acc);
     } else if (e < kGB) {
         const int f = e - kGP, tk = f / (kEmb * kPin), c = (f / kPin) % kEmb, k = f % kPin;
-        float acc = red[kPEF + (tk * kGd + kQkv + c) * kPin + k];  // F_i[c][k]
-        for (int r = 0; r < kQkv; r++) acc = fmaf(W[r * kEmb + c], red[kPEF + (tk * kGd + r) * kPin + k], acc);
+        double acc = red[kPEF + (tk * kGd + kQkv + c) * kPin + k];  // F_i[c][k]
+        for (int r = 0; r < kQkv; r++) acc = fma((double)W[r * kEmb + c], red[kPEF + (tk * kGd + r) * kPin + k], acc);
         put(acc);
     } else {
         const int f = e - kGB, tk = f / kEmb, c = f % kEmb;
-        float acc = red[kPef + tk * kGd + kQkv + c];  // f_i[c]
-        for (int r = 0; r < kQkv; r++) acc = fmaf(W[r * kEmb + c], red[kPef + tk * kGd + r], acc);
+        double acc = red[kPef + tk * kGd + kQkv + c];  // f_i[c]
+        for (int r = 0; r < kQkv; r++) acc = fma((double)W[r * kEmb + c], red[kPef + tk * kGd + r], acc);
         put(acc);
     }
 }
@@ -1398,8 +1402,10 @@ static int front_bwd(const float* ws, const float* x, int ldx, int B, int parity
                      int grid, float* red, float* grad, const FrontGradPtrs* dst, int algo, void* stream) {
     if (!ws || !x || !dh || !partial || !red || (!grad && !dst) || B < 0 || ldx < MM_OBS_DIM || grid <= 0)
         return MM_E_ARG;
+    if ((uintptr_t)red & 7) return MM_E_ARG;  // red holds the fp64 sums: 2 x mm_actor_front_partial_len() floats
     if (algo != MM_FRONT_BWD_MFMA && algo != MM_FRONT_BWD_VALU) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
+    double* red64 = reinterpret_cast<double*>(red);
     if (algo == MM_FRONT_BWD_MFMA)
         hipLaunchKernelGGL(k_front_bwd_mfma, dim3(grid), dim3(kMThreads), 0, s, ws, x, ldx, B, parity, dh, partial);
     else
@@ -1407,14 +1413,14 @@ static int front_bwd(const float* ws, const float* x, int ldx, int B, int parity
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(k_front_sum, dim3((kPartLen + kSumCols - 1) / kSumCols), dim3(kSumCols * kSumClasses), 0, s,
-                       partial, grid, red);
+                       partial, grid, red64);
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     if (grad)
-        hipLaunchKernelGGL(k_front_combine<false>, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, grad,
+        hipLaunchKernelGGL(k_front_combine<false>, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red64, grad,
                            FrontGradPtrs{});
     else
-        hipLaunchKernelGGL(k_front_combine<true>, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red, nullptr, *dst);
+        hipLaunchKernelGGL(k_front_combine<true>, dim3((kGradLen + 255) / 256), dim3(256), 0, s, ws, red64, nullptr, *dst);
     return (int)hipGetLastError();
 }
 

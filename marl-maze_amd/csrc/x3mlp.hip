@@ -57,12 +57,15 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
 
-enum { P_X3 = MM_PREC_X3, P_F16 = MM_PREC_F16 };
+enum { P_X3 = MM_PREC_X3, P_F16 = MM_PREC_F16, P_X2 = MM_PREC_X2 };
 template <int P>
 struct Prec {
-    static constexpr int kPlanes = P == P_X3 ? 3 : 1;
+    static constexpr int kPlanes = P == P_X3 ? 3 : P == P_X2 ? 2 : 1;
     static constexpr int kBlk = 512 * kPlanes;  // uint16 per (rt, ks) block
+    static constexpr bool kScaled = P != P_X3;  // operand scales / the output's cscale apply
 };
+constexpr float kX2Lo = 2048.f;         // P_X2: lo = RN16(2^11 (x - hi))
+constexpr float kX2LoInv = 1.f / 2048.f;
 
 constexpr int kBlk = 1536;  // uint16 per (rt, ks) block of P_X3: 3 planes x 512
 constexpr int kRowPad = 256;
@@ -108,6 +111,28 @@ __device__ __forceinline__ uint4 f16x8_rn(const float* v, float s) {
                       f16x2_rn(v[6] * s, v[7] * s));
 }
 
+// P_X2: two values x s -> (hi, lo) fp16 pairs, hi = RN16(x s), lo = RN16(2^11 (x s - hi)).  x s - hi is exact
+// (hi is the nearest fp16 to x s: Sterbenz), the 2^11 is exact, so lo carries the next 11 significand bits
+// and x s = hi + 2^-11 lo to 2^-22 relative while hi is normal (|x s| >= 2^-14).
+__device__ __forceinline__ void pair2(float x0, float x1, float s, uint32_t& h, uint32_t& l) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+    const f2 v = f2{x0, x1} * s;
+    const h2 hv = __builtin_convertvector(v, h2);
+    const f2 r = (v - __builtin_convertvector(hv, f2)) * kX2Lo;
+    h = __builtin_bit_cast(uint32_t, hv);
+    l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h2));
+}
+
+// 8 values -> the two 16-byte P_X2 plane pieces
+__device__ __forceinline__ void pair8(const float* v, float s, uint4& h, uint4& l) {
+    uint32_t hh[4], ll[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) pair2(v[2 * k], v[2 * k + 1], s, hh[k], ll[k]);
+    h = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+    l = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
 // the 8 values of one fragment piece -> the P planes (16 bytes each) at dst, dst + 64, ... (uint4 units)
 __device__ __forceinline__ void split2(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l);
 
@@ -120,14 +145,29 @@ __device__ __forceinline__ void store_piece(const float* v, float s, uint4* dst)
         dst[0] = make_uint4(h[0], h[1], h[2], h[3]);
         dst[64] = make_uint4(m[0], m[1], m[2], m[3]);
         dst[128] = make_uint4(l[0], l[1], l[2], l[3]);
+    } else if constexpr (P == P_X2) {
+        uint4 h, l;
+        pair8(v, s, h, l);
+        dst[0] = h;
+        dst[64] = l;
     } else {
         dst[0] = f16x8_rn(v, s);
     }
 }
 
-// one fragment product, the precision's MFMAs (P_X3: the six partial products, small terms first)
+// one fragment product, the precision's MFMAs (P_X3: the six partial products, small terms first; P_X2:
+// hi hi into acc, the cross terms hi lo + lo hi into accx -- combined by x2_combine before the epilogue)
 template <int P>
-__device__ __forceinline__ f32x4 mma(const bf16x8* a, const bf16x8* b, f32x4 acc) {
+__device__ __forceinline__ f32x4 mma(const bf16x8* a, const bf16x8* b, f32x4 acc, f32x4& accx) {
+    if constexpr (P == P_X2) {
+#define MM_H8(x) __builtin_bit_cast(f16x8, x)
+        accx = __builtin_amdgcn_mfma_f32_16x16x32_f16(MM_H8(a[1]), MM_H8(b[0]), accx, 0, 0, 0);
+        accx = __builtin_amdgcn_mfma_f32_16x16x32_f16(MM_H8(a[0]), MM_H8(b[1]), accx, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(MM_H8(a[0]), MM_H8(b[0]), acc, 0, 0, 0);
+#undef MM_H8
+        return acc;
+    }
+    (void)accx;
     if constexpr (P == P_X3) {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
@@ -139,6 +179,17 @@ __device__ __forceinline__ f32x4 mma(const bf16x8* a, const bf16x8* b, f32x4 acc
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a[0]), __builtin_bit_cast(f16x8, b[0]),
                                                      acc, 0, 0, 0);
     }
+    return acc;
+}
+
+// P_X2: the product = hi hi + 2^-11 (hi lo + lo hi), one rounding (the scaling by 2^-11 is exact)
+template <int P>
+__device__ __forceinline__ f32x4 x2_combine(f32x4 acc, f32x4 accx) {
+    if constexpr (P == P_X2) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) acc[g] = fmaf(accx[g], kX2LoInv, acc[g]);
+    }
+    (void)accx;
     return acc;
 }
 
@@ -203,11 +254,19 @@ constexpr int kWaves = X3_WAVES;  // the streaming kernel's waves per workgroup 
 constexpr int kThreads = 64 * kWaves;
 constexpr int kBM = 16 * kWaves;  // rows per workgroup: one row tile per wave
 static_assert(kBM <= kRowPad, "A row blocks must stay inside the TP row padding");
+// per precision: P_X2 holds two accumulator sets (17 column tiles: 136 registers), so its workgroups are
+// 8 waves (two per SIMD, 256 registers each) instead of 16
+template <int P>
+struct SW {
+    static constexpr int kWaves = P == P_X2 ? 8 : ::mm::x3::kWaves;
+    static constexpr int kThreads = 64 * kWaves;
+    static constexpr int kBM = 16 * kWaves;
+};
 
 template <int NT, int P = P_X3>
 struct Cfg {
     static constexpr int kPiecesB = Prec<P>::kPlanes * NT;      // 1-KiB B pieces per k-step
-    static constexpr int kPerWaveB = (kPiecesB + kWaves - 1) / kWaves;
+    static constexpr int kPerWaveB = (kPiecesB + SW<P>::kWaves - 1) / SW<P>::kWaves;
     static constexpr int kStageB = NT * Prec<P>::kBlk;          // uint16 per B stage
     static constexpr int kEpiLen = kWaves * 16 * 36 * 2;         // uint16: the waves' TP epilogue slices
     static constexpr int kLen0 = kStageB > kEpiLen ? kStageB : kEpiLen;  // stage buffer 0 doubles as epilogue
@@ -332,6 +391,14 @@ struct ASrcF32V {
             a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
             a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
             a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+        } else if constexpr (P == P_X2) {
+            uint32_t h[4], l[4];
+            pair2(r[0].x, r[0].y, scale, h[0], l[0]);
+            pair2(r[0].z, r[0].w, scale, h[1], l[1]);
+            pair2(r[1].x, r[1].y, scale, h[2], l[2]);
+            pair2(r[1].z, r[1].w, scale, h[3], l[3]);
+            a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+            a[1] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
         } else {
             const float s = scale;
             a[0] = __builtin_bit_cast(bf16x8, make_uint4(f16x2_rn(r[0].x * s, r[0].y * s), f16x2_rn(r[0].z * s, r[0].w * s),
@@ -346,7 +413,7 @@ typedef ASrcF32V<2> ASrcF32U;
 // prefetch the next step's raw A (registers) and B pieces (the other buffer;
 // the DMA issues spread over the column loop), the 6 x NT MFMAs, one barrier.
 template <int NT, int P, class AS>
-__device__ __forceinline__ void k_step(f32x4 (&acc)[NT], const AS& as, const typename AS::Raw& raw,
+__device__ __forceinline__ void k_step(f32x4 (&acc)[NT], f32x4 (&accx)[NT], const AS& as, const typename AS::Raw& raw,
                                        typename AS::Raw& rawn, const uint16_t* Bg, int nks, int ks,
                                        const uint16_t* cur, uint16_t* nxt, int wave, int lane) {
     using C = Cfg<NT, P>;
@@ -365,13 +432,13 @@ __device__ __forceinline__ void k_step(f32x4 (&acc)[NT], const AS& as, const typ
 #else
         if (false) {
 #endif
-            const int i = wave + kWaves * c;
+            const int i = wave + SW<P>::kWaves * c;
             if (i < C::kPiecesB) dma_b<P>(Bg, nks, ks + 1, i, nxt + i * 512, lane);
         }
         bf16x8 b[3];
 #pragma unroll
         for (int q = 0; q < np; q++) b[q] = b8[(c * np + q) * 64];
-        acc[c] = mma<P>(a, b, acc[c]);
+        acc[c] = mma<P>(a, b, acc[c], accx[c]);
     }
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();  // vmcnt(0): this wave's next-stage pieces and A loads landed; the barrier: every
@@ -411,7 +478,7 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
         for (int g = 0; g < 4; g++) {
             const int row = 16 * rt + rq + g, bit = 4 * c + g;
             float x = acc[c][g];
-            if (P == P_F16) x *= ep.cscale;
+            if (Prec<P>::kScaled) x *= ep.cscale;
             if (EM == EM_BWD) {
                 if (!((bits[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
             } else {
@@ -429,7 +496,7 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
             for (int g = 0; g < 4; g++) {
                 const int row = 16 * rt + rq + g;
                 if (row < M && ((bits[(4 * c + g) >> 5] >> ((4 * c + g) & 31)) & 1u))
-                    cs += P == P_F16 ? acc[c][g] * ep.cscale : acc[c][g];
+                    cs += Prec<P>::kScaled ? acc[c][g] * ep.cscale : acc[c][g];
             }
             cs += __shfl_xor(cs, 16);
             cs += __shfl_xor(cs, 32);
@@ -550,7 +617,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
         for (int g = 0; g < 4; g++) {
             const int bit = 4 * c + g;
             float x = acc[c][g];
-            if (P == P_F16) x *= ep.cscale;
+            if (Prec<P>::kScaled) x *= ep.cscale;
             if (EM == EM_BWD) {
                 const bool on = (lbits[bit >> 5] >> (bit & 31)) & 1u;
                 if (!on) x = 0.f;
@@ -596,7 +663,7 @@ __device__ unsigned long long g_x3_stamps[256 * 16 * kWaves * 8];
 #endif
 
 template <int NT, int P, class AS, class AT, int EM>
-__global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int lda, float ascale,
+__global__ __launch_bounds__(SW<P>::kThreads) void k_x3nt(const AT* __restrict__ A, int lda, float ascale,
                                                    const uint16_t* __restrict__ B, int M, int N, int K, int nks,
                                                    int nrb, int ncb, Epi ep) {
     using C = Cfg<NT, P>;
@@ -621,7 +688,7 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         const int xcd = u & 7, slot = u >> 3;
         const int rb = (slot / ncb) * 8 + xcd, cb = slot % ncb;
         if (rb >= nrb) continue;  // workgroup-uniform
-        const int rt = rb * kWaves + wave;  // this wave's row tile
+        const int rt = rb * SW<P>::kWaves + wave;  // this wave's row tile
         const int it = (u - (int)blockIdx.x) / (int)gridDim.x;
         (void)it;
         X3_STAMP(it, 0, __builtin_amdgcn_s_memtime());
@@ -636,12 +703,12 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
             sbias[t] = col < N ? ep.bias[col] : 0.f;
         }
 
-        f32x4 acc[NT];
+        f32x4 acc[NT], accx[NT];
 #pragma unroll
-        for (int c = 0; c < NT; c++) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < NT; c++) acc[c] = accx[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         typename AS::Raw r0, r1;
-        for (int i = wave; i < C::kPiecesB; i += kWaves) dma_b<P>(Bg, nks, 0, i, sB0 + i * 512, lane);
+        for (int i = wave; i < C::kPiecesB; i += SW<P>::kWaves) dma_b<P>(Bg, nks, 0, i, sB0 + i * 512, lane);
         as.load(0, r0, lane);
         __syncthreads();
         X3_STAMP(it, 1, __builtin_amdgcn_s_memtime());
@@ -649,10 +716,12 @@ __global__ __launch_bounds__(kThreads) void k_x3nt(const AT* __restrict__ A, int
         // (no wait of a B fragment read on the other buffer's DMA)
         int ks = 0;
         for (; ks + 1 < nks; ks += 2) {
-            k_step<NT, P>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
-            k_step<NT, P>(acc, as, r1, r0, Bg, nks, ks + 1, sB1, sB0, wave, lane);
+            k_step<NT, P>(acc, accx, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
+            k_step<NT, P>(acc, accx, as, r1, r0, Bg, nks, ks + 1, sB1, sB0, wave, lane);
         }
-        if (ks < nks) k_step<NT, P>(acc, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
+        if (ks < nks) k_step<NT, P>(acc, accx, as, r0, r1, Bg, nks, ks, sB0, sB1, wave, lane);
+#pragma unroll
+        for (int c = 0; c < NT; c++) acc[c] = x2_combine<P>(acc[c], accx[c]);
         X3_STAMP(it, 2, __builtin_amdgcn_s_memtime());
 
         // ---- epilogue (after the last k-step's barrier both stage buffers are free) ----
@@ -824,9 +893,9 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    f32x4 acc[TPW];
+    f32x4 acc[TPW], accx[TPW];
 #pragma unroll
-    for (int u = 0; u < TPW; u++) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < TPW; u++) acc[u] = accx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     // wave w: the run of tiles w * tpw .. + tpw - 1 (row-major over (n-tile, k-tile)), balanced
     const int ntiles = TN * NTK, first = wave * tpw, last = min(ntiles, first + tpw);
     const int tn0 = first / NTK, tk0 = first - tn0 * NTK;
@@ -861,7 +930,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
                 const bf16x8* pb = reinterpret_cast<const bf16x8*>(cur + TN * kB + tk * kB) + lane;
 #pragma unroll
                 for (int q = 0; q < np; q++) b[q] = pb[64 * q];
-                acc[u] = mma<P>(a, b, acc[u]);
+                acc[u] = mma<P>(a, b, acc[u], accx[u]);
             }
             if (++tk == NTK) {
                 tk = 0;
@@ -884,6 +953,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
     int tn = tn0, tk = tk0;
 #pragma unroll
     for (int u = 0; u < TPW; u++) {
+        acc[u] = x2_combine<P>(acc[u], accx[u]);
         if (first + u < last) {
             const int col = col0 + 16 * tk + (lane & 15);
 #pragma unroll
@@ -983,9 +1053,9 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         for (int q = 0; q < np; q++) f[q] = p[64 * q];
     };
 
-    f32x4 acc[RN * NTK + EX];
+    f32x4 acc[RN * NTK + EX], accx[RN * NTK + EX];
 #pragma unroll
-    for (int u = 0; u < RN * NTK + EX; u++) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < RN * NTK + EX; u++) acc[u] = accx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nsteps = (nrows + 31) / 32;
 #pragma unroll
     for (int q = 0; q < kPer; q++) load_piece(q, 0);
@@ -1003,7 +1073,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     // fp16 (cheap conversion, short MFMA phase): all after the MFMAs, so the loads issued at the end of the
     // previous step get the whole MFMA phase to arrive (measured: 264 x 460 415 -> 366 us; x3: 765 -> 788)
 #if !defined(WG_NO_MFMA) && !defined(WG_CONV_LATE)
-    constexpr int kDone = P == P_F16 ? 0 : ((kSlots + kEvery - 1) / kEvery < kPer ? (kSlots + kEvery - 1) / kEvery : kPer);
+    constexpr int kDone = P != P_X3 ? 0 : ((kSlots + kEvery - 1) / kEvery < kPer ? (kSlots + kEvery - 1) / kEvery : kPer);
 #else
     constexpr int kDone = 0;
 #endif
@@ -1024,7 +1094,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
             for (int tk = 0; tk < NTK; tk++) {
                 if (tk + 1 < NTK) frag(cur + (TN + tk + 1) * kB, b[(tk + 1) & 1]);  // next k-tile, ahead
 #pragma unroll
-                for (int r = 0; r < RN; r++) acc[r * NTK + tk] = mma<P>(a[r], b[tk & 1], acc[r * NTK + tk]);
+                for (int r = 0; r < RN; r++)
+                    acc[r * NTK + tk] = mma<P>(a[r], b[tk & 1], acc[r * NTK + tk], accx[r * NTK + tk]);
                 conv_at(tk);
             }
         }
@@ -1036,7 +1107,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
             bf16x8 a1[3], b1[3];
             frag(cur + tn * kB, a1);
             frag(cur + (TN + tk) * kB, b1);
-            acc[RN * NTK + e] = mma<P>(a1, b1, acc[RN * NTK + e]);
+            acc[RN * NTK + e] = mma<P>(a1, b1, acc[RN * NTK + e], accx[RN * NTK + e]);
             conv_at((RN > 0 ? NTK : 0) + e);
         }
 #endif
@@ -1050,6 +1121,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         }
         lds_barrier();
     }
+#pragma unroll
+    for (int u = 0; u < RN * NTK + EX; u++) acc[u] = x2_combine<P>(acc[u], accx[u]);
     float* out = ws + (size_t)s * N * K;
     auto put = [&](const f32x4& v, int tn, int tk) {
         const int col = col0 + 16 * tk + (lane & 15);
@@ -1136,8 +1209,9 @@ constexpr int kBresWaves = BRES_WAVES;
 struct BresPlan {
     int xcds;   // XCDs the grid spreads over (8, or 1)
     int nblk;   // column blocks
-    int ctb;    // column tiles per block (the last may have fewer)
+    int ctb;    // column tiles of the widest block (the LDS the launch reserves)
     int tiles;  // column tiles of the output
+    int tstart[9];  // block b: column tiles tstart[b] .. tstart[b + 1] - 1 (starts even when ReLU bits are involved)
     int nfull;  // 32-wide k-steps
     int half;   // 1: a final 16-wide k-step
     int first[9];  // per XCD: block b's workgroups are first[b] .. first[b + 1] - 1
@@ -1198,6 +1272,14 @@ __device__ __forceinline__ void bres_frag(const float4 (&r)[2], float s, bf16x8 
         a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
         a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
         a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    } else if constexpr (P == P_X2) {
+        uint32_t h[4], l[4];
+        pair2(r[0].x, r[0].y, s, h[0], l[0]);
+        pair2(r[0].z, r[0].w, s, h[1], l[1]);
+        pair2(r[1].x, r[1].y, s, h[2], l[2]);
+        pair2(r[1].z, r[1].w, s, h[3], l[3]);
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+        a[1] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
     } else {
         a[0] = __builtin_bit_cast(bf16x8, make_uint4(f16x2_rn(r[0].x * s, r[0].y * s), f16x2_rn(r[0].z * s, r[0].w * s),
                                                      f16x2_rn(r[1].x * s, r[1].y * s), f16x2_rn(r[1].z * s, r[1].w * s)));
@@ -1214,14 +1296,30 @@ __device__ __forceinline__ void bres_frag16(const float4& r, float s, uint2 (&a)
         a[0] = make_uint2(h[0], h[1]);
         a[1] = make_uint2(m[0], m[1]);
         a[2] = make_uint2(l[0], l[1]);
+    } else if constexpr (P == P_X2) {
+        uint32_t h[2], l[2];
+        pair2(r.x, r.y, s, h[0], l[0]);
+        pair2(r.z, r.w, s, h[1], l[1]);
+        a[0] = make_uint2(h[0], h[1]);
+        a[1] = make_uint2(l[0], l[1]);
     } else {
         a[0] = make_uint2(f16x2_rn(r.x * s, r.y * s), f16x2_rn(r.z * s, r.w * s));
     }
 }
 
 template <int P>
-__device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x4 acc) {
+__device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x4 acc, f32x4& accx) {
     typedef __attribute__((ext_vector_type(4))) short s4;
+    typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+    if constexpr (P == P_X2) {
+#define MM_H4(x) __builtin_bit_cast(h4, x)
+        accx = __builtin_amdgcn_mfma_f32_16x16x16f16(MM_H4(a[1]), MM_H4(b[0]), accx, 0, 0, 0);
+        accx = __builtin_amdgcn_mfma_f32_16x16x16f16(MM_H4(a[0]), MM_H4(b[1]), accx, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x16f16(MM_H4(a[0]), MM_H4(b[0]), acc, 0, 0, 0);
+#undef MM_H4
+        return acc;
+    }
+    (void)accx;
     if constexpr (P == P_X3) {
 #define MM_B16(x) __builtin_bit_cast(s4, x)
         acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[2]), MM_B16(b[0]), acc, 0, 0, 0);
@@ -1232,7 +1330,6 @@ __device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x
         acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(MM_B16(a[0]), MM_B16(b[0]), acc, 0, 0, 0);
 #undef MM_B16
     } else {
-        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
         acc = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a[0]), __builtin_bit_cast(h4, b[0]), acc, 0,
                                                      0, 0);
     }
@@ -1245,7 +1342,8 @@ __device__ __forceinline__ f32x4 mma16(const uint2 (&a)[3], const uint2* b, f32x
 // one 32-wide k-step: cur -> fragments, step ks + 1 -> nxt (past the last step: offsets past K, zeros),
 // the CT column tiles' MFMAs for both row tiles (each B fragment read feeds both)
 template <int P, int CT, int RT, int VW, int D = 1>
-__device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&cur)[RT][2], float4 (&nxt)[RT][2],
+__device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], f32x4 (&accx)[RT][CT], const float4 (&cur)[RT][2],
+                                          float4 (&nxt)[RT][2],
                                           const BresA& as, int ks, int K, int kq, int ctb, int c0, int ctn,
                                           float ascale, const uint16_t* sF, int lane) {
     constexpr int np = Prec<P>::kPlanes;
@@ -1269,7 +1367,7 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&c
                 for (int q = 0; q < np; q++) bb[(c + 1) & 1][q] = bp[((c + 1) * np + q) * 64];
             }
 #pragma unroll
-            for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb[c & 1], acc[r][c]);
+            for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb[c & 1], acc[r][c], accx[r][c]);
         }
     }
 #else
@@ -1285,7 +1383,7 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], const float4 (&c
             for (int q = 0; q < np; q++) bb[q] = bp[(c * np + q) * 64];
 #endif
 #pragma unroll
-            for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb, acc[r][c]);
+            for (int r = 0; r < RT; r++) acc[r][c] = mma<P>(a[r], bb, acc[r][c], accx[r][c]);
         }
     }
 #endif
@@ -1306,7 +1404,7 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
     if (wi >= pl.first[pl.nblk]) return;  // a surplus workgroup: uniform, before any barrier
     int b = 0;
     while (b + 1 < pl.nblk && wi >= pl.first[b + 1]) b++;
-    const int t0 = b * pl.ctb, ctb = min(pl.ctb, pl.tiles - t0);
+    const int t0 = pl.tstart[b], ctb = pl.tstart[b + 1] - t0;
     const int nfull = pl.nfull, half = pl.half;
     uint16_t* sF = smem;                               // [nfull][ctb][np][512]: a step's pieces at immediate offsets
     uint16_t* sT = smem + (size_t)ctb * nfull * np * 512;  // [ctb][np][256]: the 16-wide step
@@ -1368,11 +1466,11 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
         }
         for (int s = 0; s < nsb; s++) {
             const int c0 = s * CT, ctn = min(CT, ctb - c0);
-            f32x4 acc[RT][CT];
+            f32x4 acc[RT][CT], accx[RT][CT];  // accx: P_X2's cross terms (unused otherwise)
 #pragma unroll
             for (int r = 0; r < RT; r++)
 #pragma unroll
-                for (int c = 0; c < CT; c++) acc[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int c = 0; c < CT; c++) acc[r][c] = accx[r][c] = f32x4{0.f, 0.f, 0.f, 0.f};
             // A register buffers: step ks splits cur and loads a later step into another buffer, so the
             // loads stay in flight over whole steps (one buffer made the compiler copy at the loop end,
             // waiting for the loads it had just issued).  RT = 2 (x3): two buffers, one step ahead; RT = 1
@@ -1384,13 +1482,13 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
                 bres_load<RT, VW>(as, 1, K, kq, rB);
                 int ks = 0;
                 for (; ks + 3 <= nfull; ks += 3) {
-                    bres_step<P, CT, RT, VW, 2>(acc, rA, rC, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
-                    bres_step<P, CT, RT, VW, 2>(acc, rB, rA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
-                    bres_step<P, CT, RT, VW, 2>(acc, rC, rB, as, ks + 2, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW, 2>(acc, accx, rA, rC, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW, 2>(acc, accx, rB, rA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW, 2>(acc, accx, rC, rB, as, ks + 2, K, kq, ctb, c0, ctn, ascale, sF, lane);
                 }
                 const int rem = nfull - ks;  // A holds step ks, B step ks + 1
-                if (rem >= 1) bres_step<P, CT, RT, VW, 2>(acc, rA, rC, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
-                if (rem >= 2) bres_step<P, CT, RT, VW, 2>(acc, rB, rA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                if (rem >= 1) bres_step<P, CT, RT, VW, 2>(acc, accx, rA, rC, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                if (rem >= 2) bres_step<P, CT, RT, VW, 2>(acc, accx, rB, rA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
                 if (half) {  // step nfull is in A (rem 0), B (rem 1) or C (rem 2)
 #pragma unroll
                     for (int r = 0; r < RT; r++)
@@ -1401,11 +1499,11 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
                 bres_load<RT, VW>(as, 0, K, kq, rawA);
                 int ks = 0;
                 for (; ks + 2 <= nfull; ks += 2) {
-                    bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
-                    bres_step<P, CT, RT, VW>(acc, rawB, rawA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW>(acc, accx, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                    bres_step<P, CT, RT, VW>(acc, accx, rawB, rawA, as, ks + 1, K, kq, ctb, c0, ctn, ascale, sF, lane);
                 }
                 const bool odd = ks < nfull;
-                if (odd) bres_step<P, CT, RT, VW>(acc, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
+                if (odd) bres_step<P, CT, RT, VW>(acc, accx, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
                 if (half) {
 #pragma unroll
                     for (int r = 0; r < RT; r++) bres_frag16<P>(odd ? rawB[r][0] : rawA[r][0], ascale, a4[r]);
@@ -1420,10 +1518,14 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
 #pragma unroll
                         for (int q = 0; q < np; q++) bb[q] = bp[(c * np + q) * 64];
 #pragma unroll
-                        for (int r = 0; r < RT; r++) acc[r][c] = mma16<P>(a4[r], bb, acc[r][c]);
+                        for (int r = 0; r < RT; r++) acc[r][c] = mma16<P>(a4[r], bb, acc[r][c], accx[r][c]);
                     }
                 }
             }
+#pragma unroll
+            for (int r = 0; r < RT; r++)
+#pragma unroll
+                for (int c = 0; c < CT; c++) acc[r][c] = x2_combine<P>(acc[r][c], accx[r][c]);
 #pragma unroll
             for (int r = 0; r < RT; r++)
                 bres_epilogue<P, CT, EM>(acc[r], RT * u + r, t0 + c0, ctn, M, N, ep, crs, srs, sbias + 16 * c0, lane);
@@ -1455,8 +1557,8 @@ extern "C" int mm_x3_stamps_clear() {
 extern "C" long mm_x3_tp_len(int R, int C) { return (long)(rup(R, kRowPad) / 16) * (rup(C, 32) / 32) * kBlk; }
 
 extern "C" long mm_gemm_tp_len(int prec, int R, int C) {
-    if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
-    return mm_x3_tp_len(R, C) / (prec == MM_PREC_X3 ? 1 : 3);
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
+    return mm_x3_tp_len(R, C) / 3 * (prec == MM_PREC_X3 ? 3 : prec == MM_PREC_X2 ? 2 : 1);
 }
 
 extern "C" long mm_x3_mbits_len(int M) { return (long)(rup(M, kRowPad) / 16) * 64 * kMaskWords; }
@@ -1473,6 +1575,9 @@ extern "C" int mm_gemm_tp_pack(int prec, const float* X, int R, int C, int ld, i
                            total, tp);
     else if (prec == MM_PREC_F16)
         hipLaunchKernelGGL(k_tp_pack<P_F16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, X, R, C, ld, trans, nks,
+                           total, tp);
+    else if (prec == MM_PREC_X2)
+        hipLaunchKernelGGL(k_tp_pack<P_X2>, dim3(grid), dim3(256), 0, (hipStream_t)stream, X, R, C, ld, trans, nks,
                            total, tp);
     else
         return MM_E_ARG;
@@ -1497,6 +1602,8 @@ extern "C" int mm_gemm_tp_pack_multi(int prec, const mm_pack_seg_t* segs, int ns
         hipLaunchKernelGGL(k_tp_pack_multi<P_X3>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ps);
     else if (prec == MM_PREC_F16)
         hipLaunchKernelGGL(k_tp_pack_multi<P_F16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ps);
+    else if (prec == MM_PREC_X2)
+        hipLaunchKernelGGL(k_tp_pack_multi<P_X2>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ps);
     else
         return MM_E_ARG;
     return (int)hipGetLastError();
@@ -1519,13 +1626,14 @@ static int persistent_grid() {  // one 16-wave workgroup per CU
 template <int NT, int P, class AS, class AT>
 static int launch_nt(const AT* a, int lda, float ascale, const uint16_t* b, int M, int N, int K, int ncb,
                      const Epi& ep, hipStream_t s) {
+    constexpr int kT = SW<P>::kThreads;
     const int nks = rup(K, 32) / 32;
-    const int nrb = rup(M, kBM) / kBM;
-    const int grid = std::min(rup(nrb, 8) * ncb, persistent_grid());
+    const int nrb = rup(M, SW<P>::kBM) / SW<P>::kBM;
+    const int grid = std::min(rup(nrb, 8) * ncb, persistent_grid() * (P == P_X2 ? 2 : 1));
     if (ep.ctp && ep.c) return MM_E_ARG;  // one output form per launch
     if constexpr (P == P_X3) {
         if (ep.ctp) {
-            hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_TP>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M,
+            hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_TP>), dim3(grid), dim3(kT), 0, s, a, lda, ascale, b, M,
                                N, K, nks, nrb, ncb, ep);
             return (int)hipGetLastError();
         }
@@ -1533,13 +1641,13 @@ static int launch_nt(const AT* a, int lda, float ascale, const uint16_t* b, int 
         return MM_E_ARG;
     }
     if (ep.mbits_out)
-        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_FWD>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M, N,
+        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_FWD>), dim3(grid), dim3(kT), 0, s, a, lda, ascale, b, M, N,
                            K, nks, nrb, ncb, ep);
     else if (ep.mbits_in)
-        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_BWD>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M, N,
+        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_BWD>), dim3(grid), dim3(kT), 0, s, a, lda, ascale, b, M, N,
                            K, nks, nrb, ncb, ep);
     else
-        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_F32>), dim3(grid), dim3(kThreads), 0, s, a, lda, ascale, b, M, N,
+        hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_F32>), dim3(grid), dim3(kT), 0, s, a, lda, ascale, b, M, N,
                            K, nks, nrb, ncb, ep);
     return (int)hipGetLastError();
 }
@@ -1558,7 +1666,7 @@ static int dispatch_nt(const AT* a, int lda, float ascale, const uint16_t* b_tp,
     // few rows (the rollout's 4,096-8,192-row calls, the reference's 3,000-sample minibatches): too few
     // 256-row units to fill the chip, so the columns are split into 4-tile blocks (x5 workgroups at N =
     // 264).  Needs the buffer-store epilogue when bits are involved (it writes whole mask bytes per block).
-    const int nrb = rup(M, kBM) / kBM;
+    const int nrb = rup(M, SW<P>::kBM) / SW<P>::kBM;
     if (tiles > 4 && !ep.ctp && (ep.bufok || (!ep.mbits_in && !ep.mbits_out)) && 2L * nrb * ncb <= persistent_grid()) {
         NT = 4;
         ncb = (tiles + 3) / 4;
@@ -1605,37 +1713,61 @@ constexpr int kBresMinRows = 16384;
 // wave units: C_NARROW two row tiles x 6 column tiles (acc 48 registers; each B fragment read feeds two
 // tiles) -- x3, and f16 up to 6 tiles; C_WIDE (f16) one row tile x up to 17 column tiles (acc 68: the
 // whole 264-wide output per wave, A read once)
-enum { C_NARROW = 0, C_WIDE = 1 };
-template <int C> struct BresCfg { static constexpr int CT = C == C_NARROW ? 6 : 17, RT = C == C_NARROW ? 2 : 1; };
+// C_PAIR (x2): one row tile x up to 9 column tiles (two accumulator sets: 72 registers), the widest block
+// two B planes leave room for at K = 264
+enum { C_NARROW = 0, C_WIDE = 1, C_PAIR = 2 };
+template <int C>
+struct BresCfg {
+    static constexpr int CT = C == C_NARROW ? 6 : C == C_WIDE ? 17 : 9, RT = C == C_NARROW ? 2 : 1;
+};
 
 // The column blocks and the per-XCD workgroup split (see k_bres); false: the shape does not fit.
 static bool bres_plan(int prec, int M, int N, int K, int lda, int ldc, bool bits, BresPlan& pl, int& cfg) {
     // A and C through buffer resources (num_records < 2^31, in-range offsets < 2^31 = kBufOOB)
     if (M < kBresMinRows || (size_t)M * lda * 4 >= ((size_t)1 << 31) || (size_t)(M + 16) * ldc * 4 >= ((size_t)1 << 31))
         return false;
-    const int np = prec == MM_PREC_X3 ? 3 : 1;
+    const int np = prec == MM_PREC_X3 ? 3 : prec == MM_PREC_X2 ? 2 : 1;
     const int tiles = (N + 15) / 16;
     const int nks = rup(K, 32) / 32, rem = K % 32;
     pl.half = rem != 0 && rem <= 16;
     pl.nfull = nks - pl.half;
     const long tile_bytes = (long)np * (pl.nfull * 1024L + pl.half * 512L) + 64;  // + the bias columns
     int cmax = (int)((160L * 1024) / tile_bytes);
-    if (cmax >= tiles) cmax = tiles;
-    else if (bits) cmax &= ~1;  // blocks start at even tiles: whole mask bytes per block
+    if (prec == MM_PREC_X2) cmax = std::min(cmax, BresCfg<C_PAIR>::CT);  // one sub-block per wave
     if (cmax < 1 || pl.nfull < 1) return false;
-    int nblk = (tiles + cmax - 1) / cmax;
-    int ctb = (tiles + nblk - 1) / nblk;
-    if (bits && nblk > 1 && (ctb & 1)) ctb++;
-    if (ctb > cmax) return false;
-    nblk = (tiles + ctb - 1) / ctb;
-    if (nblk > 1 && ctb < 4) return false;  // A re-read per block: x3 at K = 460 (3 tiles) measured slower
-    // f16 at K = 460 (two blocks: A of 460 columns read twice): the streaming kernel measured 0.81x
-    if (prec == MM_PREC_F16 && nblk > 1 && K > 288) return false;
-    if (nblk > kBresMaxBlk) return false;
-    cfg = (prec == MM_PREC_F16 && ctb > BresCfg<C_NARROW>::CT) ? C_WIDE : C_NARROW;
+    // blocks: as few as fit, then the narrowest widest block; every block but the last holds e tiles, and
+    // with ReLU bits e is even (blocks start at even tiles: whole mask bytes per block) -- x3 at K = 264:
+    // 6 + 6 + 5, x2: 8 + 9
+    int nblk = 0, e_best = 0, ctb = 0;
+    for (int nb = (tiles + cmax - 1) / cmax; nb <= kBresMaxBlk && !nblk; nb++) {
+        if (nb == 1) {
+            nblk = 1;
+            ctb = e_best = tiles;
+            break;
+        }
+        for (int e = cmax; e >= 1; e--) {
+            if (bits && (e & 1)) continue;
+            const int last = tiles - e * (nb - 1);
+            if (last < 1 || last > cmax) continue;
+            const int wmax = std::max(e, last);
+            if (!nblk || wmax < ctb) {
+                nblk = nb;
+                ctb = wmax;
+                e_best = e;
+            }
+        }
+    }
+    if (!nblk) return false;
+    if (nblk > 1 && std::min(e_best, tiles - e_best * (nblk - 1)) < 4 && prec != MM_PREC_X2)
+        return false;  // A re-read per block: x3 at K = 460 (3 tiles) measured slower
+    // f16 / x2 at K = 460 (blocks re-reading A of 460 columns): the streaming kernel measured faster (f16 0.81x)
+    if (prec != MM_PREC_X3 && nblk > 1 && K > 288) return false;
+    cfg = prec == MM_PREC_X2 ? C_PAIR : (prec == MM_PREC_F16 && ctb > BresCfg<C_NARROW>::CT) ? C_WIDE : C_NARROW;
     pl.nblk = nblk;
     pl.ctb = ctb;
     pl.tiles = tiles;
+    for (int bk = 0; bk <= kBresMaxBlk; bk++) pl.tstart[bk] = std::min(tiles, bk * e_best);
+    pl.tstart[nblk] = tiles;
     const int G = persistent_grid();
     pl.xcds = G % 8 == 0 ? 8 : 1;
     const int per = G / pl.xcds;
@@ -1646,7 +1778,7 @@ static bool bres_plan(int prec, int M, int N, int K, int lda, int ldc, bool bits
     for (int left = per - nblk; left > 0; left--) {
         int best = 0;
         for (int bk = 1; bk < nblk; bk++) {
-            const int tb = std::min(ctb, tiles - bk * ctb), tbest = std::min(ctb, tiles - best * ctb);
+            const int tb = pl.tstart[bk + 1] - pl.tstart[bk], tbest = pl.tstart[best + 1] - pl.tstart[best];
             if ((long)tb * w[best] > (long)tbest * w[bk]) best = bk;
         }
         w[best]++;
@@ -1686,9 +1818,14 @@ static int dispatch_bres_c(const float* a, int lda, float ascale, const uint16_t
 template <int P, int VW>
 static int dispatch_bres(const float* a, int lda, float ascale, const uint16_t* b, int M, int N, int K,
                          const BresPlan& pl, int cfg, const Epi& ep, hipStream_t s) {
-    if constexpr (P == P_F16)
-        if (cfg == C_WIDE) return dispatch_bres_c<P, C_WIDE, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
-    return dispatch_bres_c<P, C_NARROW, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+    if constexpr (P == P_X2) {
+        (void)cfg;
+        return dispatch_bres_c<P, C_PAIR, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+    } else {
+        if constexpr (P == P_F16)
+            if (cfg == C_WIDE) return dispatch_bres_c<P, C_WIDE, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+        return dispatch_bres_c<P, C_NARROW, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+    }
 }
 
 static int check_common(const uint16_t* b_tp, int M, int N, int K, const float* mask, int ldm, float* c, int ldc,
@@ -1719,7 +1856,7 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
                         void* stream) {
     int e = check_common(b_tp, M, N, K, mask, ldm, c, ldc, c_tp);
     if (e) return e;
-    if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (ascale != 1.f || cscale != 1.f)) return MM_E_ARG;  // the split is exact: no scaling
     const bool v4 = !(K & 3) && !(lda & 3) && !((uintptr_t)a & 15);
     const bool v2 = !(K & 1) && !(lda & 1) && !((uintptr_t)a & 7);
@@ -1754,12 +1891,18 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
         if (prec == MM_PREC_X3)
             return v4 ? dispatch_bres<P_X3, 4>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s)
                       : dispatch_bres<P_X3, 2>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s);
+        if (prec == MM_PREC_X2)
+            return v4 ? dispatch_bres<P_X2, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s)
+                      : dispatch_bres<P_X2, 2>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s);
         return v4 ? dispatch_bres<P_F16, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s)
                   : dispatch_bres<P_F16, 2>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s);
     }
     if (prec == MM_PREC_X3)
         return v4 ? dispatch_nt<P_X3, ASrcF32>(a, lda, 1.f, b_tp, M, N, K, ep, s)
                   : dispatch_nt_u<P_X3>(a, lda, 1.f, b_tp, M, N, K, ep, s);
+    if (prec == MM_PREC_X2)
+        return v4 ? dispatch_nt<P_X2, ASrcF32>(a, lda, ascale, b_tp, M, N, K, ep, s)
+                  : dispatch_nt_u<P_X2>(a, lda, ascale, b_tp, M, N, K, ep, s);
     return v4 ? dispatch_nt<P_F16, ASrcF32>(a, lda, ascale, b_tp, M, N, K, ep, s)
               : dispatch_nt_u<P_F16>(a, lda, ascale, b_tp, M, N, K, ep, s);
 }
@@ -1808,7 +1951,7 @@ static WgPlan wg_plan(int prec, int M, int N, int K) {
     // column blocks: at most 20 tiles per wave (the register budget of 2 waves per SIMD) and two image sets
     // within 160 KiB of LDS; a slice's blocks share its dY rows through the XCD's L2
     p.ncb = (tk_all + kWgMaxT - 1) / kWgMaxT;
-    const int kb = prec == MM_PREC_X3 ? 1536 : 512;
+    const int kb = prec == MM_PREC_X3 ? 1536 : prec == MM_PREC_X2 ? 1024 : 512;
     auto fits = [&](int ncb) {
         const int ntk = (tk_all + ncb - 1) / ncb;
         return p.TN * ntk <= kWgWaves * 20 && 2 * (p.TN + ntk) * kb * 2 <= 160 * 1024;
@@ -1833,7 +1976,7 @@ static WgPlan wg_plan(int prec, int M, int N, int K) {
 extern "C" long mm_gemm_wgrad_ws_len(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0) return 0;
     long n = 0;  // the larger of the two precisions' plans
-    for (int prec : {MM_PREC_X3, MM_PREC_F16}) {
+    for (int prec : {MM_PREC_X3, MM_PREC_F16, MM_PREC_X2}) {
         const WgPlan p = wg_plan(prec, M, N, K);
         n = std::max(n, (long)p.nslices * N * K);
     }
@@ -1901,14 +2044,15 @@ static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int ldd
 #endif
     if ((size_t)M * lddy * 4 >= ((size_t)1 << 31) || (size_t)M * ldx * 4 >= ((size_t)1 << 31))
         return 1;  // loads through buffer resources (num_records < 2^31): the generic kernel
-    return prec == MM_PREC_X3 ? launch_rect_p<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
-                              : launch_rect_p<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    return prec == MM_PREC_X3   ? launch_rect_p<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
+           : prec == MM_PREC_X2 ? launch_rect_p<P_X2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s)
+                                : launch_rect_p<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
 }
 
 static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
                       float cscale, float* ws, float* dw, void* stream) {
     if (M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
-    if (prec != MM_PREC_X3 && prec != MM_PREC_F16) return MM_E_ARG;
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (dscale != 1.f || cscale != 1.f)) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
     if (M == 0) return dw ? (int)hipMemsetAsync(dw, 0, sizeof(float) * (size_t)N * K, s) : MM_E_ARG;
@@ -1916,8 +2060,10 @@ static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const f
     const WgPlan p = wg_plan(prec, M, N, K);
     if (!p.TPW) return MM_E_ARG;
     int e = launch_wgrad_rect(prec, p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
-    if (e == 1) e = prec == MM_PREC_X3 ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
-                                       : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    if (e == 1)
+        e = prec == MM_PREC_X3   ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
+            : prec == MM_PREC_X2 ? launch_wgrad<P_X2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s)
+                                 : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
     if (e) return e;
     const long n = (long)N * K;
     if (!dw) return 0;  // mm_gemm_wgrad_partials: the caller reduces (mm_wsum_multi)
@@ -1932,7 +2078,8 @@ extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, 
 }
 
 extern "C" int mm_gemm_wgrad_slices(int prec, int M, int N, int K) {
-    if (M <= 0 || N <= 0 || K <= 0 || (prec != MM_PREC_X3 && prec != MM_PREC_F16)) return MM_E_ARG;
+    if (M <= 0 || N <= 0 || K <= 0 || (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2))
+        return MM_E_ARG;
     const WgPlan p = wg_plan(prec, M, N, K);
     return p.TPW ? p.nslices : MM_E_ARG;
 }

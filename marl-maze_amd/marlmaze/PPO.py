@@ -38,6 +38,7 @@ from .networks import Actor, Critic
 from .vecmaze import VecMaze
 
 MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
+FP32_GEMM = "x3"  # the default fp32-class GEMM precision of dtype="f32" (networks.GEMM_PRECISIONS)
 
 
 def _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip):
@@ -113,7 +114,12 @@ class PPO:
         if dtype not in ("f32", "f16"):
             raise ValueError(f"dtype must be 'f32' or 'f16', not {dtype!r}")
         self.dtype = dtype
-        prec = "x3" if dtype == "f32" else "f16"
+        # the fp32-class GEMM arithmetic: "x2" (two fp16 planes, three MFMAs per product) or "x3" (three bf16
+        # planes, six); MARLMAZE_FP32_GEMM overrides the default for A/B runs
+        prec = (os.environ.get("MARLMAZE_FP32_GEMM", FP32_GEMM) if dtype == "f32" else "f16")
+        if prec not in ("x2", "x3", "f16"):
+            raise ValueError(f"MARLMAZE_FP32_GEMM must be 'x2' or 'x3', not {prec!r}")
+        self.gemm_prec = prec
         self.actor = Actor([264, 264, 264], parity_mode=parity_mode, gemm_prec=prec).to(self.device)
         self.critic = Critic(agent_amount, hidden_sizes=[64, 64], gemm_prec=prec).to(self.device)
         torch.random.set_rng_state(g)
@@ -263,9 +269,21 @@ class PPO:
 
     def _rollout_steps(self, b, n, T, offset_dev=None):
         head_w, head_b = self.actor.heads()
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        # the critic and the actor read the same observations and nothing of each other: with the rollout
+        # captured (a few thousand mazes, every kernel latency-bound) the critic runs on a side stream beside
+        # the actor -- two branches of the graph
+        side = self._critic_stream() if (self.graph_rollout and cur is not None) else None
         for t in range(T):
             obs_t = b["obs"][t]
-            b["val"][t] = self.critic(obs_t).view(n)
+            if side is not None:
+                side.wait_stream(cur)  # obs[t] written by the previous step's env kernel
+                with torch.cuda.stream(side):
+                    self.critic.value_into(obs_t, b["val"][t])
+            elif cur is not None:
+                self.critic.value_into(obs_t, b["val"][t])
+            else:
+                b["val"][t] = self.critic(obs_t).view(n)
             # actor trunk, then heads + sampling fused (PPO.py:170-186; ops.head_sample)
             h = self.actor.trunk(obs_t.view(2 * n, 65))
             ops.head_sample(h, head_w, head_b, b["masks"][t].view(2 * n, 6), self.sample_seed,
@@ -285,6 +303,8 @@ class PPO:
                                reward=b["rew"][t], done=b["done"][t], ep_stats=b["stats"][t], events=(e0, e1))
                 self.venv.reset_done(obs=b["obs"][t + 1], masks=b["masks"][t + 1])
                 ev.append((e0, e1))
+        if side is not None:
+            cur.wait_stream(side)  # every value written before the GAE reads them
         last = None
         if self.bootstrap:
             b["last_val"].copy_(self.critic(b["obs"][T]).view(n))
@@ -292,6 +312,11 @@ class PPO:
         ops.gae(b["rew"], b["val"], b["done"], last_value=last, gamma=self.discount_rate, lam=self.lam,
                 adv=b["adv"], rtg=b["rtg"])
         return b
+
+    def _critic_stream(self):
+        if getattr(self, "_cstream", None) is None:
+            self._cstream = torch.cuda.Stream(device=self.device)
+        return self._cstream
 
     def _carry_over(self):
         """The next batch starts from the last observation (episodes continue)."""

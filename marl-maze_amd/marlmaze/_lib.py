@@ -46,7 +46,7 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi")
 VERSION = 303  # mm_version() this binding is written for
 
-PREC_X3, PREC_F16 = 0, 1  # MM_PREC_*
+PREC_X3, PREC_F16, PREC_X2 = 0, 1, 2  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
 FRONT_FWD = {"row1": 0, "row2": 1}  # MM_FRONT_FWD_*
 GEMM_ALGO = {"auto": 0, "stream": 1}  # MM_GEMM_*

@@ -136,7 +136,7 @@ class _FusedFront(torch.autograd.Function):
         grid = _front_bwd_grid(B, x.device)
         plen = L.mm_actor_front_partial_len()
         partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
-        red = torch.empty(plen, dtype=torch.float32, device=x.device)
+        red = torch.empty(plen, dtype=torch.float64, device=x.device)  # the fp64 sums
         g = torch.empty(L.mm_actor_front_grad_len(), dtype=torch.float32, device=x.device)
         _lib.check(L.mm_actor_front_bwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(ctx.parity), _lib.ptr(dh),
                                            _lib.ptr(partial), grid, _lib.ptr(red), _lib.ptr(g),
@@ -163,10 +163,11 @@ def front_params(projection, attention):
 # networks.py:35-41) and the critic (130 -> 64 -> 64 -> 1, networks.py:87-102)
 # run on the hand-written GEMMs of csrc/x3mlp.hip at every row count, forward
 # and backward:
-# * precision "x3" (default): fp32-class -- each operand split exactly into
-#   three bf16 parts, six bf16 MFMA products kept; "f16": one fp16 MFMA product
-#   per element (BASELINE configs[4]).  Storage, master weights and Adam stay
-#   fp32 in both.  The actor heads always run at x3: the rollout's fused
+# * precision "x3": fp32-class -- each operand split exactly into three bf16
+#   parts, six bf16 MFMA products kept; "x2": fp32-class on two fp16 parts per
+#   operand (x = hi + 2^-11 lo, 22 significand bits), three f16 MFMA products;
+#   "f16": one fp16 MFMA product per element (BASELINE configs[4]).  Storage,
+#   master weights and Adam stay fp32 in all three.  The actor heads always run at x3: the rollout's fused
 #   head + sampler kernel computes them in fp32, and the update's log-probs
 #   must be those of the same logits.
 # * weights are packed per call into fragment-order planes (tiny); the
@@ -176,13 +177,13 @@ def front_params(projection, attention):
 #   per-tile column sums of the next layer's bias gradient (summed by mm_colsum);
 # * weight gradients dW = dY^T X run on mm_gemm_wgrad (row-slice partials
 #   summed in a fixed order).
-# The fp16 backward GEMMs scale dY by 2^floor(log2 M): the losses are means
+# The fp16 / x2 backward GEMMs scale dY by 2^floor(log2 M): the losses are means
 # over M rows, so per-row gradients are ~1/M, and the scale keeps them in
 # fp16's normal range; the results are unscaled (powers of two: exact).
 # Shapes the engine does not take (a non-ReLU activation, layers wider than
 # 272, inputs not a multiple of 4 wide) -- none of which the reference builds --
 # run as plain torch ops, with a warning on the GPU.
-GEMM_PRECISIONS = ("x3", "f16")
+GEMM_PRECISIONS = ("x3", "x2", "f16")
 _MAX_WIDTH = 272
 _WARNED = set()
 
@@ -201,8 +202,8 @@ def _warn_torch_path(what):
 
 
 def _grad_scale(M, prec):
-    """The power-of-two dY scale of the fp16 backward GEMMs (1 for x3)."""
-    return float(2.0 ** int(math.floor(math.log2(max(int(M), 1))))) if prec == "f16" else 1.0
+    """The power-of-two dY scale of the fp16-operand backward GEMMs, f16 and x2 (1 for x3)."""
+    return float(2.0 ** int(math.floor(math.log2(max(int(M), 1))))) if prec in ("f16", "x2") else 1.0
 
 
 def _wgrad(dy, x, prec, out=None):
@@ -325,14 +326,14 @@ class _EngineActor(torch.autograd.Function):
         return (None, dx, dwh, dbh, *grads)
 
 
-def _critic_fwd(x, params, prec, need_bits):
+def _critic_fwd(x, params, prec, need_bits, out=None):
     """networks.py:96-102 on the engine: x [M, 130] (8-byte rows) -> ReLU(64) ->
-    ReLU(64) -> V [M, 1]."""
+    ReLU(64) -> V [M, 1] (into ``out`` [M, 1] when given)."""
     from . import x3
 
     w0, b0, w1, b1, w2, b2 = params
     hs, bits = _mlp_fwd(x, (w0, w1), (b0, b1), prec, need_bits)
-    return x3.gemm(hs[-1], x3.pack(w2, prec=prec), bias=b2), hs, bits
+    return x3.gemm(hs[-1], x3.pack(w2, prec=prec), bias=b2, out=out), hs, bits
 
 
 def _critic_bwd(hs, bits, params, dv, prec, outs=None):
@@ -533,16 +534,23 @@ def _front_fwd(x, parity, params):
     """The fused front-end forward (no autograd): (workspace, h [B, 460])."""
     from . import _lib
 
+    from . import x3
+
     L = _lib.lib()
     B = x.shape[0]
-    ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device=x.device)
-    ptrs = [p.data_ptr() for p in params]
-    wp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
-    bp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[FEATURE_AMOUNT:2 * FEATURE_AMOUNT])
-    wq, wk, wv = params[2 * FEATURE_AMOUNT:]
     stream = _lib.stream_ptr()
-    _lib.check(L.mm_actor_front_prep(wp, bp, _lib.ptr(wq), _lib.ptr(wk), _lib.ptr(wv), _lib.ptr(ws), stream),
-               "mm_actor_front_prep")
+
+    def prep():  # the folded maps depend on the weights only: once per rollout inside x3.cached_packs()
+        ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device=x.device)
+        ptrs = [p.data_ptr() for p in params]
+        wp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
+        bp = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[FEATURE_AMOUNT:2 * FEATURE_AMOUNT])
+        wq, wk, wv = params[2 * FEATURE_AMOUNT:]
+        _lib.check(L.mm_actor_front_prep(wp, bp, _lib.ptr(wq), _lib.ptr(wk), _lib.ptr(wv), _lib.ptr(ws), stream),
+                   "mm_actor_front_prep")
+        return ws
+
+    ws = x3.cached_value("front_prep", params, prep)
     h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
     _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
                                        _lib.FRONT_FWD[FRONT_FWD_ALGO], stream), "mm_actor_front_fwd_ex")
@@ -560,7 +568,7 @@ def _front_bwd_to(ws, x, parity, dh, grads):
     grid = _front_bwd_grid(B, x.device)
     plen = L.mm_actor_front_partial_len()
     partial = torch.empty((grid, plen), dtype=torch.float32, device=x.device)
-    red = torch.empty(plen, dtype=torch.float32, device=x.device)
+    red = torch.empty(plen, dtype=torch.float64, device=x.device)  # the fp64 sums
     assert all(g.is_contiguous() for g in grads)
     ptrs = [g.data_ptr() for g in grads]
     gw = (ctypes.c_void_p * FEATURE_AMOUNT)(*ptrs[:FEATURE_AMOUNT])
@@ -621,6 +629,17 @@ class Critic(nn.Module):
         return F.linear(x, self.layers[-1].weight, self.layers[-1].bias)
 
     # ---- the update's explicit forward / backward (no autograd; GPU) ----
+    @torch.no_grad()
+    def value_into(self, x, out):
+        """V(x) written into out ([M] or [M, 1] fp32, contiguous) -- the rollout's per-step values without a
+        copy (GPU engine shapes only)."""
+        x = x.reshape(x.shape[0], -1)
+        if not self._engine(x):
+            out.copy_(self(x).reshape(out.shape))
+            return out
+        _critic_fwd(x, self._params(), self.gemm_prec, False, out=out.view(-1, 1))
+        return out
+
     def train_forward(self, x):
         """x [M, agents * 65] f32 on the GPU -> (V [M, 1], saved state)."""
         x = x.reshape(-1, self.agent_amount * OBS_SPACE).contiguous()

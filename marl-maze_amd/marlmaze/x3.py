@@ -11,7 +11,7 @@ import torch
 from . import _lib
 
 
-PRECS = {"x3": _lib.PREC_X3, "f16": _lib.PREC_F16}
+PRECS = {"x3": _lib.PREC_X3, "f16": _lib.PREC_F16, "x2": _lib.PREC_X2}
 
 
 class TP:
@@ -49,6 +49,7 @@ class cached_packs:
     def __enter__(self):
         if _CACHE_DEPTH[0] == 0:
             _PACK_CACHE.clear()
+            _DERIVED.clear()
         _CACHE_DEPTH[0] += 1
         return self
 
@@ -56,7 +57,24 @@ class cached_packs:
         _CACHE_DEPTH[0] -= 1
         if _CACHE_DEPTH[0] == 0:
             _PACK_CACHE.clear()
+            _DERIVED.clear()
         return False
+
+
+_DERIVED = {}  # cached_value(): (tag, keys of the inputs, generation) -> result, dropped with the scope
+
+
+def cached_value(tag, tensors, make):
+    """make() once per cached_packs() scope for unchanged ``tensors`` (data_ptr, version counter and the
+    invalidate_packs() generation all equal), e.g. the actor front-end's folded-map workspace, which depends
+    only on the weights; outside a scope, make() every call."""
+    if _CACHE_DEPTH[0] == 0:
+        return make()
+    key = (tag, tuple((id(t), t.data_ptr(), t._version) for t in tensors), _GENERATION[0])
+    hit = _DERIVED.get(key)
+    if hit is None:
+        hit = _DERIVED[key] = make()
+    return hit
 
 
 def _cache_get(x, key):

@@ -128,7 +128,7 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_data_parallel_update_equals_single_process(tmp_path, golden, world):
     """``world`` gloo ranks, each with 1/world of the batch and its own shuffle,
     give the same losses and parameters as one process whose minibatches are
@@ -168,7 +168,7 @@ def test_data_parallel_update_equals_single_process(tmp_path, golden, world):
     ag = PPO(2, batch_size=world * local_bs, lr=1e-6, device="cpu", load=False, verbose=False, save=False)
     hist = ag.update(*(torch.as_tensor(data[k]) for k in ("obs", "act", "logp", "masks", "adv", "val")),
                      index_list=np.asarray(glob))
-    np.testing.assert_allclose(got[0]["hist"][:, :2], hist.numpy()[:, :2], rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(got[0]["hist"][:, :2], hist.numpy()[:, :2], rtol=1e-5, atol=1e-6)
     for k, v in ag.actor.state_dict().items():
         np.testing.assert_allclose(got[0][k], v.numpy(), rtol=0, atol=3e-6)
     for k, v in ag.critic.state_dict().items():

@@ -10,6 +10,7 @@
 Tolerances, relative to sum |a b| per output element (the bound any
 reordering of an fp32 sum obeys at ~n eps):
   x3 (bf16x3, fp32-class): 1e-6 (measured 2-4e-7; the fp32 library GEMMs 3e-7);
+  x2 (fp16 hi + 2^-11 lo pairs, fp32-class): 1e-6 (operands to 2^-22 relative; the sum in fp32);
   f16 (one fp16 product, operands rounded to 11 bits): 2e-3 (two roundings of
   2^-12 each, plus the fp32 sum).
 """
@@ -20,14 +21,14 @@ from marlmaze import x3
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"x3": 1e-6, "f16": 2e-3}
+TOL = {"x3": 1e-6, "x2": 1e-6, "f16": 2e-3}
 
 
 def _rel_err(got, ref, scale):
     return ((got.double() - ref).abs() / scale.clamp_min(1e-30)).max().item()
 
 
-@pytest.mark.parametrize("prec", ["x3", "f16"])
+@pytest.mark.parametrize("prec", ["x3", "x2", "f16"])
 @pytest.mark.parametrize("M,N,K", [(419430, 264, 264), (70001, 264, 460), (40000, 6, 264), (209715, 64, 130),
                                    (30000, 64, 64), (30000, 1, 64), (100, 264, 264), (1, 6, 264), (37, 5, 9),
                                    (1, 264, 460), (300, 264, 264), (6000, 264, 460), (8192, 264, 264),
@@ -37,7 +38,7 @@ def test_wgrad_matches_fp64(prec, M, N, K):
     dy = torch.randn(M, N, device="cuda", generator=g)
     x = torch.randn(M, K, device="cuda", generator=g)
     dscale = 1.0
-    if prec == "f16":  # gradients of a mean over M rows are ~1/M: scaled into the fp16 normal range
+    if prec != "x3":  # gradients of a mean over M rows are ~1/M: scaled into the fp16 normal range
         dy *= 1.0 / M
         dscale = float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
     dw = x3.wgrad(dy, x, prec=prec, dscale=dscale)
@@ -69,7 +70,7 @@ def algo(request):
     x3.set_algo(prev)
 
 
-@pytest.mark.parametrize("prec", ["x3", "f16"])
+@pytest.mark.parametrize("prec", ["x3", "x2", "f16"])
 @pytest.mark.parametrize("M,N,K", [(40000, 264, 460), (40000, 264, 264), (40000, 6, 264), (40000, 64, 130),
                                    (40000, 1, 64), (777, 64, 64), (40000, 460, 264), (16411, 264, 264),
                                    (20000, 96, 52),
@@ -122,6 +123,27 @@ def test_gemm_rejects_bad_shapes():
         x3.gemm(a, x3.pack(torch.randn(264, 130, device="cuda")))
     with pytest.raises(_lib.MMError):  # x3 operands are exact splits: no scaling
         x3.gemm(torch.randn(100, 64, device="cuda"), x3.pack(torch.randn(8, 64, device="cuda")), ascale=2.0)
+
+
+@pytest.mark.parametrize("M,N,K", [(40000, 264, 264), (40000, 264, 460), (3000, 264, 264)])
+def test_x2_dynamic_range(M, N, K, algo):
+    """x2 keeps 22 significand bits for 2^-14 <= |x s| <= 2^15 (the 2^11-scaled lo part stays out of the fp16
+    subnormals): operands spread over 2^-12 .. 2^12 per element, forward and scaled input-gradient forms and the
+    weight gradient, at the fp32-class bar."""
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    spread = lambda *shape: torch.randn(*shape, device="cuda", generator=g) * torch.exp2(  # noqa: E731
+        torch.randint(-12, 13, shape, device="cuda", generator=g).float())
+    a = spread(M, K)
+    w = spread(N, K) * 2.0**-6
+    y = x3.gemm(a, x3.pack(w, prec="x2"))
+    ref = a.double() @ w.double().t()
+    assert _rel_err(y, ref, a.double().abs() @ w.double().abs().t()) < TOL["x2"]
+    dy = spread(M, N) / M
+    s = float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
+    dx = x3.gemm(dy, x3.pack(w, trans=True, prec="x2"), ascale=s)
+    assert _rel_err(dx, dy.double() @ w.double(), dy.double().abs() @ w.double().abs()) < TOL["x2"]
+    dw = x3.wgrad(dy, a, prec="x2", dscale=s)
+    assert _rel_err(dw, dy.double().t() @ a.double(), dy.double().abs().t() @ a.double().abs()) < TOL["x2"]
 
 
 @pytest.mark.parametrize("algo", ["auto", "stream"], indirect=True)

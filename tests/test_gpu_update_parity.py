@@ -330,8 +330,8 @@ def test_config1_rollout_and_update_4096_mazes(golden):
     actor.load_state_dict({k: v.cpu() for k, v in ag.actor.state_dict().items()})
     critic.load_state_dict({k: v.cpu() for k, v in ag.critic.state_dict().items()})
     # rollout actor inputs are the 4 facing one-hots (quirk Q1), so the minibatch's gradient sums
-    # collapse onto 4 activation vectors and cancel; see the module doc for the 2e-5 here
-    _step_and_compare(ag, actor, critic, batch, "configs[1]", grad_rel=2e-5)
+    # collapse onto 4 activation vectors and cancel (see the module doc): held to the default 1e-5
+    _step_and_compare(ag, actor, critic, batch, "configs[1]")
 
 
 def test_main_py_hyperparameters_minibatch(golden):
