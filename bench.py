@@ -273,6 +273,7 @@ def main():
             "horizon": T, "global_batch": batch_global, "minibatch": batch_global // 5,
             "minibatch_steps_per_iter": minibatches_per_iter, "parallelism": f"dp{world}",
             "rollout": "HIP graph replay" if graph else "stream launches",
+            "gemm": agent.gemm_prec,
             "parity_mode": not a.no_parity,
         },
         "ppo_updates_per_sec": minibatches_per_iter * a.steps / elapsed,
@@ -281,7 +282,8 @@ def main():
         "roofline": {
             "kernel": "k_step (mm_env_step)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,
-            "alg_bytes_per_env_step": alg_bytes, "launch_us": env_step_ms * 1e3, "launches": len(step_ms),
+            "alg_bytes_per_env_step": alg_bytes, "launch_us": env_step_ms * 1e3,
+            "launch_us_median": float(np.median(step_ms)) * 1e3, "launches": len(step_ms),
             "timed_in": "the timed region" if not graph else "one instrumented rollout after the timed region",
         },
     }

@@ -32,13 +32,12 @@ import random
 import numpy as np
 import torch
 
-from . import ops, update, x3
+from . import networks, ops, update, x3
 from .dist import DP
 from .networks import Actor, Critic
 from .vecmaze import VecMaze
 
 MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
-FP32_GEMM = "x3"  # the default fp32-class GEMM precision of dtype="f32" (networks.GEMM_PRECISIONS)
 
 
 def _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip):
@@ -114,11 +113,9 @@ class PPO:
         if dtype not in ("f32", "f16"):
             raise ValueError(f"dtype must be 'f32' or 'f16', not {dtype!r}")
         self.dtype = dtype
-        # the fp32-class GEMM arithmetic: "x2" (two fp16 planes, three MFMAs per product) or "x3" (three bf16
-        # planes, six); MARLMAZE_FP32_GEMM overrides the default for A/B runs
-        prec = (os.environ.get("MARLMAZE_FP32_GEMM", FP32_GEMM) if dtype == "f32" else "f16")
-        if prec not in ("x2", "x3", "f16"):
-            raise ValueError(f"MARLMAZE_FP32_GEMM must be 'x2' or 'x3', not {prec!r}")
+        # the fp32-class GEMM arithmetic: networks.FP32_GEMM, "x2" (two fp16 planes, three MFMAs per product)
+        # unless MARLMAZE_FP32_GEMM=x3 (three bf16 planes, six)
+        prec = networks.FP32_GEMM if dtype == "f32" else "f16"
         self.gemm_prec = prec
         self.actor = Actor([264, 264, 264], parity_mode=parity_mode, gemm_prec=prec).to(self.device)
         self.critic = Critic(agent_amount, hidden_sizes=[64, 64], gemm_prec=prec).to(self.device)

@@ -17,7 +17,7 @@ feature its own slice (what the code evidently intended).
 """
 import ctypes
 import math
-import os as _os
+import os
 
 import numpy as np
 import torch
@@ -83,7 +83,7 @@ class m_Attention(nn.Module):
 _CUS = {}
 # the front-end backward's attention products: "mfma" (fp32 MFMA tiles, csrc/actor_front.hip
 # k_front_bwd_mfma; the default) or "valu" (fp32 FMA, one lane per token, k_front_bwd)
-FRONT_BWD_ALGO = _os.environ.get("MARLMAZE_FRONT_BWD", "mfma")
+FRONT_BWD_ALGO = os.environ.get("MARLMAZE_FRONT_BWD", "mfma")
 
 
 def _front_bwd_grid(B, dev):
@@ -98,7 +98,7 @@ def _front_bwd_grid(B, dev):
     return grid
 # the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads) or "row1" (one per lane);
 # bit-identical outputs (csrc/actor_front.hip k_front_fwd2 / k_front_fwd)
-FRONT_FWD_ALGO = _os.environ.get("MARLMAZE_FRONT_FWD", "row1")
+FRONT_FWD_ALGO = os.environ.get("MARLMAZE_FRONT_FWD", "row1")
 
 
 def _cu_count(dev):
@@ -184,6 +184,11 @@ def front_params(projection, attention):
 # 272, inputs not a multiple of 4 wide) -- none of which the reference builds --
 # run as plain torch ops, with a warning on the GPU.
 GEMM_PRECISIONS = ("x3", "x2", "f16")
+# the fp32-class arithmetic of the product (x2: half the MFMAs of x3 at the same 1e-6 GEMM bar, 0.76x the time
+# of x3 over the update's shapes, tools/bench_prec.py); MARLMAZE_FP32_GEMM=x3 selects the other for A/B runs
+FP32_GEMM = os.environ.get("MARLMAZE_FP32_GEMM", "x2")
+if FP32_GEMM not in ("x2", "x3"):
+    raise ValueError(f"MARLMAZE_FP32_GEMM must be 'x2' or 'x3', not {FP32_GEMM!r}")
 _MAX_WIDTH = 272
 _WARNED = set()
 
@@ -388,9 +393,10 @@ class Actor(nn.Module):
     """networks.py:13-48.  forward(x) -> [move_logits [B,5], mark_logit [B,1]]."""
 
     def __init__(self, hidden_sizes=(164, 164, 164, 164, 164), activation=nn.ReLU, parity_mode=True,
-                 gemm_prec="x3"):
+                 gemm_prec=None):
         super().__init__()
         hidden_sizes = list(hidden_sizes)
+        gemm_prec = FP32_GEMM if gemm_prec is None else gemm_prec
         assert gemm_prec in GEMM_PRECISIONS
         self.gemm_prec = gemm_prec  # the MLP GEMMs' precision on the GPU (the front-end stays fp32)
         self.projection = Projection(parity_mode)
@@ -583,9 +589,10 @@ def _front_bwd_to(ws, x, parity, dh, grads):
 class Critic(nn.Module):
     """networks.py:84-106.  forward(x [.., agents, 65]) -> V [B, 1]."""
 
-    def __init__(self, agent_amount, hidden_sizes=(128, 128), activation=nn.ReLU, gemm_prec="x3"):
+    def __init__(self, agent_amount, hidden_sizes=(128, 128), activation=nn.ReLU, gemm_prec=None):
         super().__init__()
         hidden_sizes = list(hidden_sizes)
+        gemm_prec = FP32_GEMM if gemm_prec is None else gemm_prec
         assert gemm_prec in GEMM_PRECISIONS
         self.gemm_prec = gemm_prec  # the GEMMs' precision on the GPU
         self.layers = nn.ModuleList()

@@ -69,15 +69,16 @@ def test_zero_grad_set_to_none_rebinds_flat_buffer(golden):
     ag.actor.load_state_dict({k[6:]: torch.as_tensor(fx[k]).cuda() for k in fx.files if k.startswith("actor/")})
     ag.critic.load_state_dict({k[7:]: torch.as_tensor(fx[k]).cuda() for k in fx.files if k.startswith("critic/")})
     batch = tuple(torch.as_tensor(fx[k]).cuda() for k in ("obs", "actions", "old_logp", "advs", "rtgs", "masks"))
+    params = list(ag.actor.parameters()) + list(ag.critic.parameters())
     ag.minibatch_grads(*batch)
-    ref = ag.flat.grad.clone()
-    ag.flat.grad.fill_(float("nan"))
+    ref = [p.grad.clone() for p in params]
+    ag.flat.grad.fill_(float("nan"))  # (the alignment padding between parameters stays NaN: never written)
     ag.actor.zero_grad()  # set_to_none=True: the .grad views are gone
     ag.critic.zero_grad()
-    assert all(p.grad is None for p in ag.actor.parameters())
+    assert all(p.grad is None for p in params)
     ag.minibatch_grads(*batch)
-    assert torch.equal(ag.flat.grad, ref)
     lo, hi = ag.flat.grad.data_ptr(), ag.flat.grad.data_ptr() + 4 * ag.flat.numel
-    for p in list(ag.actor.parameters()) + list(ag.critic.parameters()):
-        assert lo <= p.grad.data_ptr() < hi
-    assert np.isfinite(ref.cpu().numpy()).all()
+    for p, r in zip(params, ref):
+        assert lo <= p.grad.data_ptr() < hi  # a view of the flat buffer again
+        assert torch.equal(p.grad, r) and torch.equal(ag.flat.moment_view(ag.flat.grad, p), r)
+        assert np.isfinite(r.cpu().numpy()).all()

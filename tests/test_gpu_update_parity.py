@@ -14,18 +14,14 @@ The bar (BASELINE north star): 1e-5 relative.  Stated per quantity:
   cancel ~100:1 over the minibatch, and torch-CPU fp32 lands 1.2e-5..2.8e-5
   of max|g| away from fp64 there (tools/diag_grad_err.py).  On such a tensor
   the bound is twice the reference's own fp32 error instead.
-  Exception, stated: BASELINE configs[1]'s rollout minibatch, 2e-5.  There
-  the actor sees only the 4 facing one-hots (Q1), every gradient sum over the
-  26,214 rows collapses onto 4 activation vectors, and the rounding of the
-  MFMA GEMMs -- whose adder trees truncate inside each instruction
-  (tools/mfma_round.hip: in-group products are cut toward zero below 2^-24 of
-  the group's largest; a -0.017..-0.14 eps mean error per dot product,
-  tools/diag_x3_bias.py) -- is coherent across rows instead of averaging out:
-  in round 2, 6 of 65 tensors landed at 1.04e-5..1.28e-5 of max|g| (the fp32
-  library GEMMs on the same data: 1.08e-5..1.14e-5); with the round-3 update
-  path one is left, projection.layers.0.bias at 1.27e-5 (the same with the
-  reference's exact softmax steps in the front-end backward), the fp32 CPU
-  oracle at <= 7.6e-6;
+  BASELINE configs[1]'s rollout minibatch is held to the same 1e-5.  There the
+  actor sees only the 4 facing one-hots (Q1), every gradient sum over the
+  26,214 rows collapses onto 4 activation vectors, and rounding that is
+  coherent across rows does not average out: in round 3 one tensor,
+  projection.layers.0.bias, landed at 1.27e-5 of max|g| (its gradient f_0 +
+  Wqkv^T e_0 cancels).  The front-end's partial sums are now reduced and
+  combined in fp64 (k_front_sum / k_front_combine), and the trunk runs on the
+  x2 arithmetic: no tensor is above 1e-5.
 * the Adam step, per parameter tensor: Delta p = p_after - p_before agrees
   with the fp64 oracle's Adam step at 1e-5 lr + 1 ulp of the fp32 parameter
   wherever the clipped gradient is >= 1e-4 (Adam's first step is ~ -lr g/|g|,

@@ -1,6 +1,6 @@
 """One actor-trunk GEMM shape launched repeatedly (for rocprofv3 --pmc passes).
 
-SHAPE=NxK (default 264x264), M rows (default 419,430), PREC=x3|f16, FORM=fwd (bias + ReLU +
+SHAPE=NxK (default 264x264), M rows (default 419,430), PREC=x3|x2|f16, FORM=fwd (bias + ReLU +
 bits out) | bwd (bits in + column sums) | plain; MARLMAZE_GEMM_BRES=0 selects k_x3nt.
 """
 import os
@@ -27,7 +27,7 @@ def main():
     if N <= 272:
         x3.gemm(a, w, bias=bias, relu=True, mbits_out=mb, out=out)
     cs = x3.colsum_buf(M, N, "cuda")
-    ascale = 1.0 if prec == "x3" else 1.0
+    ascale = 1.0
 
     def one():
         if form == "fwd":
