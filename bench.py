@@ -209,10 +209,14 @@ def main():
 
     if not graph:
         agent.step_events = []  # instrumented env steps inside the timed region (uncaptured rollout)
-    upd_ev = []
+    upd_ev, roll_ev = [], []
     t0 = time.time()
     for _ in range(a.steps):
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record()
         b = agent.rollout()
+        r1.record()
+        roll_ev.append((r0, r1))
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         B = T * n
@@ -236,6 +240,7 @@ def main():
         torch.cuda.synchronize()
     step_ms = [s.elapsed_time(e) for s, e in agent.step_events]
     upd_ms = [s.elapsed_time(e) for s, e in upd_ev]
+    roll_ms = [s.elapsed_time(e) for s, e in roll_ev]
     env_step_ms = float(np.mean(step_ms))
     H = 2 * a.size - 1
     alg_bytes = H * H + 703  # layout + marks + agents r/w + maze r/w + actions + obs + masks + reward + done
@@ -279,6 +284,8 @@ def main():
         "ppo_updates_per_sec": minibatches_per_iter * a.steps / elapsed,
         "update_ms_per_iter": float(np.mean(upd_ms)),
         "rollout_env_steps_per_sec": total_steps / (elapsed - sum(upd_ms) * 1e-3),
+        "rollout_ms_per_iter": float(np.mean(roll_ms)),  # GPU time of rollout() + GAE (events around it)
+        "rollout_us_per_step": float(np.mean(roll_ms)) * 1e3 / T,
         "roofline": {
             "kernel": "k_step (mm_env_step)", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "traffic_source": traffic_src,

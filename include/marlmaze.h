@@ -411,6 +411,13 @@ int mm_head_sample_ex(const float* h, int ldh, int K, const float* w, const floa
  * 0, K <= 1024, 16-byte aligned rows); M * ldh * 4 < 2^31. */
 int mm_heads_fwd(const float* h, int ldh, int K, const float* w, const float* b, int M, float* logits, void* stream);
 
+/* The critic's value in one launch (networks.py:87-102, inference: PPO.get_batch's per-step
+ * self.critic(obs), PPO.py:111): v [M] = w2 . ReLU(w1 ReLU(w0 x + b0) + b1) + b2 for x [M, K0] (row
+ * stride ldx), w0 [H0, K0], w1 [H1, H0], w2 [1, H1] (nn.Linear layouts), on the fp32 MFMA (exact fmaf
+ * chains, fp32 accumulation).  K0 <= 192, H0 = H1 = 64 (PPO's Critic); other shapes return MM_E_ARG. */
+int mm_critic_value(const float* x, int ldx, int K0, int M, int H0, int H1, const float* w0, const float* b0,
+                    const float* w1, const float* b1, const float* w2, const float* b2, float* v, void* stream);
+
 /* Actor front-end, fused (networks.py:31-34,51-82): the 23 feature embeddings
  * (Projection; parity != 0 keeps quirk Q1, every embedding reads x[:, 0:d_i]),
  * Q/K/V, softmax(QK^T/sqrt(10))V and the residual.

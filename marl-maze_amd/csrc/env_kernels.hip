@@ -491,6 +491,41 @@ __global__ __launch_bounds__(64) void k_reset(mm_env_t env, const uint8_t* __res
     }
 }
 
+// The done-list reset of the rollout (mm_env_step's auto-reset, mm_env_reset_done) in ONE launch: workgroup b
+// (one wavefront) regenerates its list entries b, b + G, ... one after another (k_reset's work), then its lanes
+// form their reset observations in parallel, lane j for its j-th maze (k_reset_obs's work), after a barrier
+// that orders the new layouts / maze records before the reads; the last workgroup clears the list.  Per step
+// at a few thousand mazes the two launches were two latency floors (~5 us each plus the gap between them).
+__global__ __launch_bounds__(64) void k_reset_list(mm_env_t env, float* obs, uint8_t* masks) {
+    __shared__ GenLds g;
+    const int count = min(env.work[0], env.n);
+    const int G = gridDim.x, per = (count + G - 1) / G;  // list entries per workgroup (round-robin)
+    for (int j0 = 0; j0 < per; j0 += 64) {
+        const int jn = min(64, per - j0);
+        for (int j = j0; j < j0 + jn; j++) {
+            const int k = blockIdx.x + G * j;  // workgroup-uniform
+            if (k < count) {
+                reset_one(env, g, env.work[kListOff + k]);
+                __syncthreads();
+            }
+        }
+        __syncthreads();  // the wavefront's layout / maze-record writes before the lanes observe them
+        const int k = blockIdx.x + G * (j0 + (int)threadIdx.x);
+        if ((int)threadIdx.x < jn && k < count) reset_observe(env, env.work[kListOff + k], obs, masks);
+        __syncthreads();
+    }
+    // done list consumed: the LAST block to finish clears the counter (every block read work[0] above, before
+    // taking its ticket); kernel boundaries order this against the next k_step
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int ticket = atomicAdd(&env.work[1], 1);
+        if (ticket == (int)gridDim.x - 1) {
+            env.work[0] = 0;
+            env.work[1] = 0;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // step (one thread per maze)
 // ---------------------------------------------------------------------------
@@ -831,6 +866,10 @@ extern "C" int mm_env_seed(const mm_env_t* env, const uint64_t* seeds, void* str
 
 static int launch_reset(const mm_env_t* env, const uint8_t* mask, int use_list, float* obs, uint8_t* masks,
                         hipStream_t s) {
+    if (use_list) {
+        hipLaunchKernelGGL(k_reset_list, dim3(512), dim3(64), 0, s, *env, obs, masks);
+        return (int)hipGetLastError();
+    }
     int grid = use_list ? 512 : (env->n < 16384 ? env->n : 16384);
     hipLaunchKernelGGL(k_reset, dim3(grid), dim3(64), 0, s, *env, mask, use_list, obs, masks);
     hipError_t e = hipGetLastError();

@@ -38,6 +38,9 @@ from .networks import Actor, Critic
 from .vecmaze import VecMaze
 
 MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
+# the captured rollout's critic on a side stream (a parallel branch of the graph): MARLMAZE_ROLLOUT_SIDE=0 keeps
+# it on the main stream (A/B)
+ROLLOUT_SIDE_STREAM = os.environ.get("MARLMAZE_ROLLOUT_SIDE", "1") != "0"
 
 
 def _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip):
@@ -270,7 +273,8 @@ class PPO:
         # the critic and the actor read the same observations and nothing of each other: with the rollout
         # captured (a few thousand mazes, every kernel latency-bound) the critic runs on a side stream beside
         # the actor -- two branches of the graph
-        side = self._critic_stream() if (self.graph_rollout and cur is not None) else None
+        side = (self._critic_stream() if (self.graph_rollout and cur is not None and ROLLOUT_SIDE_STREAM)
+                else None)
         for t in range(T):
             obs_t = b["obs"][t]
             if side is not None:

@@ -43,7 +43,7 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
            "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
-           "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi")
+           "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi", "mm_critic_value")
 VERSION = 303  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16, PREC_X2 = 0, 1, 2  # MM_PREC_*
@@ -142,6 +142,8 @@ def lib():
         L.mm_head_sample.restype = i32
         L.mm_heads_fwd.argtypes = [P, i32, i32, P, P, i32, P, P]
         L.mm_heads_fwd.restype = i32
+        L.mm_critic_value.argtypes = [P, i32, i32, i32, i32, i32, P, P, P, P, P, P, P, P]
+        L.mm_critic_value.restype = i32
         L.mm_head_sample_ex.argtypes = [P, i32, i32, P, P, P, i32, u64, u64, P, P, P, P, P, P]
         L.mm_head_sample_ex.restype = i32
         L.mm_x3_tp_len.argtypes = [i32, i32]

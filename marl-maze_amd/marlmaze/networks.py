@@ -640,9 +640,19 @@ class Critic(nn.Module):
     def value_into(self, x, out):
         """V(x) written into out ([M] or [M, 1] fp32, contiguous) -- the rollout's per-step values without a
         copy (GPU engine shapes only)."""
+        from . import _lib
+
         x = x.reshape(x.shape[0], -1)
         if not self._engine(x):
             out.copy_(self(x).reshape(out.shape))
+            return out
+        w0, b0, w1, b1, w2, b2 = self._params()
+        if (len(self.layers) == 3 and w0.shape[0] == 64 and w1.shape == (64, 64) and w2.shape == (1, 64)
+                and x.shape[1] <= 192 and out.is_contiguous() and self.gemm_prec != "f16"):
+            # the three layers in one launch on the fp32 MFMA (mm_critic_value)
+            _lib.check(_lib.lib().mm_critic_value(_lib.ptr(x), x.stride(0), x.shape[1], x.shape[0], 64, 64,
+                                                   *(_lib.ptr(t) for t in (w0, b0, w1, b1, w2, b2)), _lib.ptr(out),
+                                                   _lib.stream_ptr()), "mm_critic_value")
             return out
         _critic_fwd(x, self._params(), self.gemm_prec, False, out=out.view(-1, 1))
         return out

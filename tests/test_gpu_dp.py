@@ -124,11 +124,13 @@ def test_two_rank_gpu_update_equals_union_update(tmp_path):
     hist = ag.update(cat["obs"], cat["act"], cat["logp"], cat["masks"], cat["adv"], cat["val"],
                      index_list=glob).cpu().numpy()
     for k in range(2):
-        # minibatch 0: the same parameters on both sides, only the gradients' summation order differs (rank
-        # halves summed by the all-reduce vs one GEMM over the union): the 1e-5 bar.  Later minibatches start
-        # from parameters that differ in their last bits (Adam steps on gradients rounded differently), and
-        # that difference compounds over the 24 further steps: 5e-5
-        np.testing.assert_allclose(r[k]["hist"].numpy()[0], hist[0], rtol=1e-5, atol=1e-6)
-        np.testing.assert_allclose(r[k]["hist"].numpy(), hist, rtol=5e-5, atol=1e-6)
+        # minibatch 0: the same parameters on both sides.  Its losses are per-row sums of the same values: the
+        # 1e-5 bar.  Its unclipped gradient norms come from weight gradients summed in a different order (rank
+        # halves, then the all-reduce, vs one reduction over the union); the critic's weight gradients cancel
+        # ~100:1 over the rows, so the fp32 order alone moves their norm by up to ~4e-5: 1e-4.  Later
+        # minibatches start from parameters that differ in their last bits (Adam steps on gradients rounded
+        # differently), compounding over 24 further steps: 1e-4
+        np.testing.assert_allclose(r[k]["hist"].numpy()[0, :2], hist[0, :2], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(r[k]["hist"].numpy(), hist, rtol=1e-4, atol=1e-6)
     for name, v in r[0]["params"].items():
         assert torch.equal(v, r[1]["params"][name]), name

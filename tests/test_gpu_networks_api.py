@@ -82,3 +82,26 @@ def test_zero_grad_set_to_none_rebinds_flat_buffer(golden):
         assert lo <= p.grad.data_ptr() < hi  # a view of the flat buffer again
         assert torch.equal(p.grad, r) and torch.equal(ag.flat.moment_view(ag.flat.grad, p), r)
         assert np.isfinite(r.cpu().numpy()).all()
+
+
+@pytest.mark.parametrize("M", [1, 63, 4096, 70001])
+def test_fused_critic_value_matches_oracle(golden, M):
+    """mm_critic_value (the rollout's per-step V, networks.py:87-102) against the fp64 oracle critic: the three
+    layers on the fp32 MFMA in one launch, at 1e-5 of max |V| (ragged row counts: partial 16-row tiles and
+    workgroups)."""
+    from marlmaze.networks import Critic
+
+    fx = golden("nets")
+    cr = Critic(2, hidden_sizes=[64, 64]).cuda()
+    cr.load_state_dict({k[7:]: torch.as_tensor(fx[k]).cuda() for k in fx.files if k.startswith("critic/")})
+    obs = torch.as_tensor(fx["obs"]).reshape(-1, 130)
+    g = torch.Generator().manual_seed(M)
+    x = obs[torch.randint(0, obs.shape[0], (M,), generator=g)] + 0.1 * torch.randn(M, 130, generator=g)
+    v = torch.full((M,), float("nan"), device="cuda")
+    cr.value_into(x.cuda(), v)
+    oc = oppo.OCritic()
+    oc.load_state_dict({k[7:]: torch.as_tensor(fx[k]) for k in fx.files if k.startswith("critic/")})
+    with torch.no_grad():
+        ref = oc.double()(x.double()).squeeze(-1)
+    err = (v.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * ref.abs().max().item() + 1e-6, err
