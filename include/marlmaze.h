@@ -414,7 +414,7 @@ int mm_heads_fwd(const float* h, int ldh, int K, const float* w, const float* b,
 /* The critic's value in one launch (networks.py:87-102, inference: PPO.get_batch's per-step
  * self.critic(obs), PPO.py:111): v [M] = w2 . ReLU(w1 ReLU(w0 x + b0) + b1) + b2 for x [M, K0] (row
  * stride ldx), w0 [H0, K0], w1 [H1, H0], w2 [1, H1] (nn.Linear layouts), on the fp32 MFMA (exact fmaf
- * chains, fp32 accumulation).  K0 <= 192, H0 = H1 = 64 (PPO's Critic); other shapes return MM_E_ARG. */
+ * chains, fp32 accumulation).  K0 <= 132, H0 = H1 = 64 (PPO's Critic); other shapes return MM_E_ARG. */
 int mm_critic_value(const float* x, int ldx, int K0, int M, int H0, int H1, const float* w0, const float* b0,
                     const float* w1, const float* b1, const float* w2, const float* b2, float* v, void* stream);
 

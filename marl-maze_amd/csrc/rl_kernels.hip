@@ -549,79 +549,73 @@ __global__ __launch_bounds__(256) void k_ppo_loss_bwd(const float* __restrict__ 
 // ---------------------------------------------------------------------------
 // The critic's value, fused (networks.py:87-102 forward, inference only): V = w2 . ReLU(W1 ReLU(W0 x + b0) + b1)
 // + b2 for x [M, K0], hidden widths 64 and 64, in ONE launch on the fp32 MFMA (v_mfma_f32_16x16x4_f32: an exact
-// fmaf chain per output, no operand split).  A wave owns 16 rows: its x rows are staged in LDS (coalesced
-// 16-byte loads), layer 0 is 4 column tiles x ceil(K0 / 4) k-steps with W0 read from LDS, the hidden rows go
-// back through LDS into the A-operand layout for layer 1 (4 tiles x 16 k-steps), and the value head is a
-// cross-lane dot product.  The rollout calls it once per step: at a few thousand mazes the three GEMM
-// launches it replaces were three latency floors.
+// fmaf chain per output, no operand split).  One wavefront per 16 rows, no LDS staging of the weights: each lane
+// issues ALL its operand loads up front -- its 4 x ceil(K0 / 4) W0 values, 4 x 16 W1 values and ceil(K0 / 4) x
+// values (the weights are L2-resident, 50 KB read by every wave) -- so the launch pays one memory round trip,
+// not one per k-step or per staged element (an LDS-staged form measured 20-40 us at 4,096 rows; the three
+// GEMM launches it replaces ~20 us plus two gaps).  The hidden rows go through 4 KB of LDS into the A-operand
+// layout of layer 1; the value head is a cross-lane dot product in a fixed order.
 // ---------------------------------------------------------------------------
-constexpr int kCvH = 64;                 // hidden width (PPO's Critic: hidden_sizes [64, 64])
-constexpr int kCvMaxK = 192;             // K0 limit (the reference's 130 observations x 2 agents / 2 ... = 130)
-constexpr int kCvWaves = 4;              // 64 rows per workgroup
-constexpr int kCvXp = kCvMaxK + 4;       // LDS row pitch of the staged x rows (floats)
-constexpr int kCvHp = kCvH + 4;          // LDS row pitch of the hidden rows
+constexpr int kCvH = 64;       // hidden width (PPO's Critic: hidden_sizes [64, 64])
+constexpr int kCvMaxK = 132;   // K0 limit (the reference's 2 x 65 observations = 130): 33 k-steps in registers
+constexpr int kCvMaxS = kCvMaxK / 4;
+constexpr int kCvHp = kCvH + 4;  // LDS row pitch of the hidden rows (64 banks: conflict-free A reads)
 
 typedef __attribute__((ext_vector_type(4))) float cv_f32x4;
 
-__global__ __launch_bounds__(64 * kCvWaves) void k_critic_value(const float* __restrict__ x, int ldx, int K0, int M,
-                                                                 const float* __restrict__ w0,
-                                                                 const float* __restrict__ b0,
-                                                                 const float* __restrict__ w1,
-                                                                 const float* __restrict__ b1,
-                                                                 const float* __restrict__ w2,
-                                                                 const float* __restrict__ b2, float* __restrict__ v) {
-    __shared__ float sw0[kCvH * kCvXp];          // W0 [64][K0] (pitch kCvXp, zero past K0)
-    __shared__ float sw1[kCvH * kCvHp];          // W1 [64][64]
-    __shared__ float sx[kCvWaves][16 * kCvXp];   // each wave's x rows, later its hidden rows (pitch kCvHp)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int K4 = (K0 + 3) & ~3;
-    for (int e = threadIdx.x; e < kCvH * K4; e += blockDim.x) {
-        const int r = e / K4, c = e - r * K4;
-        sw0[r * kCvXp + c] = c < K0 ? w0[(size_t)r * K0 + c] : 0.f;
+__global__ __launch_bounds__(64) void k_critic_value(const float* __restrict__ x, int ldx, int K0, int M,
+                                                     const float* __restrict__ w0, const float* __restrict__ b0,
+                                                     const float* __restrict__ w1, const float* __restrict__ b1,
+                                                     const float* __restrict__ w2, const float* __restrict__ b2,
+                                                     float* __restrict__ v) {
+    __shared__ float hs[16 * kCvHp];
+    const int lane = threadIdx.x, c16 = lane & 15, q = lane >> 4;
+    const int row0 = blockIdx.x * 16;
+    const int S0 = (K0 + 3) >> 2;
+    // operands (MFMA 16x16x4: A = row c16, k = 4 s + q; B = output column c16, same k); out-of-range reads are
+    // zeros (rows past M, columns past K0)
+    const int xr = min(row0 + c16, M - 1);
+    float xa[kCvMaxS], wa[4][kCvMaxS], wb[4][kCvH / 4];
+#pragma unroll
+    for (int s = 0; s < kCvMaxS; s++) {
+        const int k = 4 * s + q;
+        const bool ok = s < S0 && k < K0;
+        xa[s] = ok ? x[(size_t)xr * ldx + k] : 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; t++) wa[t][s] = ok ? w0[(size_t)(16 * t + c16) * K0 + k] : 0.f;
     }
-    for (int e = threadIdx.x; e < kCvH * kCvH; e += blockDim.x) sw1[(e >> 6) * kCvHp + (e & 63)] = w1[e];
-    const int row0 = (blockIdx.x * kCvWaves + wave) * 16;
-    float* xs = sx[wave];
-    // the wave's 16 rows (rows past M: zeros), columns up to K4 (zero past K0)
-    for (int e = lane; e < 16 * K4; e += 64) {
-        const int r = e / K4, c = e - r * K4;
-        xs[r * kCvXp + c] = (row0 + r < M && c < K0) ? x[(size_t)(row0 + r) * ldx + c] : 0.f;
-    }
-    __syncthreads();
-    const int c16 = lane & 15, q = lane >> 4;
-    // layer 0: C[i][j] = sum_k x[i][k] W0[j][k]; A: row c16, k = 4 s + q; B: column c16 (W0 row), same k
+#pragma unroll
+    for (int s = 0; s < kCvH / 4; s++)
+#pragma unroll
+        for (int t = 0; t < 4; t++) wb[t][s] = w1[(16 * t + c16) * kCvH + 4 * s + q];
+    // layer 0
     cv_f32x4 h[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) h[t] = cv_f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < K4 / 4; s++) {
-        const float a = xs[c16 * kCvXp + 4 * s + q];
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-            h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sw0[(16 * t + c16) * kCvXp + 4 * s + q], h[t], 0, 0, 0);
-    }
-    // bias + ReLU; lane holds rows 4 q + g, column 16 t + c16 -> the hidden rows in LDS (the wave's x is dead)
-    __builtin_amdgcn_wave_barrier();
+    for (int s = 0; s < kCvMaxS; s++)
+        if (s < S0) {  // wave-uniform
+#pragma unroll
+            for (int t = 0; t < 4; t++) h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[t][s], h[t], 0, 0, 0);
+        }
+    // bias + ReLU; lane holds rows 4 q + g, column 16 t + c16 -> LDS, read back as layer 1's A operand
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const float bb = b0[16 * t + c16];
 #pragma unroll
-        for (int g = 0; g < 4; g++) xs[(4 * q + g) * kCvHp + 16 * t + c16] = fmaxf(h[t][g] + bb, 0.f);
+        for (int g = 0; g < 4; g++) hs[(4 * q + g) * kCvHp + 16 * t + c16] = fmaxf(h[t][g] + bb, 0.f);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // layer 1
+    __syncthreads();
 #pragma unroll
     for (int t = 0; t < 4; t++) h[t] = cv_f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int s = 0; s < kCvH / 4; s++) {
-        const float a = xs[c16 * kCvHp + 4 * s + q];
 #pragma unroll
-        for (int t = 0; t < 4; t++)
-            h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, sw1[(16 * t + c16) * kCvHp + 4 * s + q], h[t], 0, 0, 0);
+    for (int s = 0; s < kCvH / 4; s++) {
+        const float a = hs[c16 * kCvHp + 4 * s + q];
+#pragma unroll
+        for (int t = 0; t < 4; t++) h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[t][s], h[t], 0, 0, 0);
     }
-    // value head: V[row] = b2 + sum_j ReLU(h1 + b1)[row][j] w2[j]; this lane's 4 rows x its 4 columns, then the
-    // sum over the 16 lanes sharing the rows (columns c16) -- a fixed order
+    // value head: V[row] = b2 + sum_j ReLU(h1 + b1)[row][j] w2[j]: this lane's 4 rows x its 4 columns, then the
+    // sum over the 16 lanes sharing the rows -- a fixed order
     float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -642,6 +636,7 @@ __global__ __launch_bounds__(64 * kCvWaves) void k_critic_value(const float* __r
         }
     }
 }
+
 }  // namespace mm
 
 using namespace mm;
@@ -749,8 +744,7 @@ extern "C" int mm_critic_value(const float* x, int ldx, int K0, int M, int H0, i
         return MM_E_ARG;
     if (H0 != mm::kCvH || H1 != mm::kCvH) return MM_E_ARG;  // the reference critic's [64, 64]
     if (M == 0) return 0;
-    const int rows = 16 * mm::kCvWaves;
-    hipLaunchKernelGGL(mm::k_critic_value, dim3((M + rows - 1) / rows), dim3(64 * mm::kCvWaves), 0,
-                       (hipStream_t)stream, x, ldx, K0, M, w0, b0, w1, b1, w2, b2, v);
+    hipLaunchKernelGGL(mm::k_critic_value, dim3((M + 15) / 16), dim3(64), 0, (hipStream_t)stream, x, ldx, K0, M, w0,
+                       b0, w1, b1, w2, b2, v);
     return (int)hipGetLastError();
 }

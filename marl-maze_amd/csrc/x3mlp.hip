@@ -1710,6 +1710,17 @@ extern "C" int mm_gemm_nt_algo(int algo) {
 }
 
 constexpr int kBresMinRows = 16384;
+// the B-resident kernel's row threshold: kBresMinRows, or MARLMAZE_BRES_MIN_ROWS (A/B runs of the small-M
+// calls: the rollout's 4,096-8,192-row GEMMs)
+static int bres_min_rows() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("MARLMAZE_BRES_MIN_ROWS");
+        v = e ? atoi(e) : kBresMinRows;
+        if (v < 1) v = 1;
+    }
+    return v;
+}
 // wave units: C_NARROW two row tiles x 6 column tiles (acc 48 registers; each B fragment read feeds two
 // tiles) -- x3, and f16 up to 6 tiles; C_WIDE (f16) one row tile x up to 17 column tiles (acc 68: the
 // whole 264-wide output per wave, A read once)
@@ -1724,7 +1735,7 @@ struct BresCfg {
 // The column blocks and the per-XCD workgroup split (see k_bres); false: the shape does not fit.
 static bool bres_plan(int prec, int M, int N, int K, int lda, int ldc, bool bits, BresPlan& pl, int& cfg) {
     // A and C through buffer resources (num_records < 2^31, in-range offsets < 2^31 = kBufOOB)
-    if (M < kBresMinRows || (size_t)M * lda * 4 >= ((size_t)1 << 31) || (size_t)(M + 16) * ldc * 4 >= ((size_t)1 << 31))
+    if (M < bres_min_rows() || (size_t)M * lda * 4 >= ((size_t)1 << 31) || (size_t)(M + 16) * ldc * 4 >= ((size_t)1 << 31))
         return false;
     const int np = prec == MM_PREC_X3 ? 3 : prec == MM_PREC_X2 ? 2 : 1;
     const int tiles = (N + 15) / 16;
@@ -1966,7 +1977,8 @@ static WgPlan wg_plan(int prec, int M, int N, int K) {
             p.TPW = t;
             break;
         }
-    // about one unit per CU: slices of whole 32-row steps
+    // about one unit per CU: slices of whole 32-row steps (a floor of 512 rows per slice, to shrink the slices'
+    // partials at BASELINE configs[1]'s 52,428-row minibatch, measured slower: 24.6 vs 23.5 ms per update)
     const int want = std::max(1, std::min((M + 31) / 32, persistent_grid() / p.ncb));
     p.rows = rup((M + want - 1) / want, 32);
     p.nslices = std::max(1, (M + p.rows - 1) / p.rows);

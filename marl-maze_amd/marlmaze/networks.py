@@ -648,8 +648,9 @@ class Critic(nn.Module):
             return out
         w0, b0, w1, b1, w2, b2 = self._params()
         if (len(self.layers) == 3 and w0.shape[0] == 64 and w1.shape == (64, 64) and w2.shape == (1, 64)
-                and x.shape[1] <= 192 and out.is_contiguous() and self.gemm_prec != "f16"):
-            # the three layers in one launch on the fp32 MFMA (mm_critic_value)
+                and x.shape[1] <= 132 and out.is_contiguous()):
+            # the three layers in one launch on the fp32 MFMA (mm_critic_value; also for the fp16 networks: the
+            # rollout's values are then fp32-class, the update's critic runs in fp16)
             _lib.check(_lib.lib().mm_critic_value(_lib.ptr(x), x.stride(0), x.shape[1], x.shape[0], 64, 64,
                                                    *(_lib.ptr(t) for t in (w0, b0, w1, b1, w2, b2)), _lib.ptr(out),
                                                    _lib.stream_ptr()), "mm_critic_value")
