@@ -239,17 +239,22 @@ __device__ __forceinline__ float dot4(const float* a, const float* __restrict__ 
     return acc.x + acc.y;
 }
 
+// acc += p * v; N % 4 == 0: packed FMAs on aligned accumulator pairs with p broadcast (per element the
+// same fmaf as the scalar form: bit-identical, half the instructions)
 template <int N>
-__device__ __forceinline__ void axpy4(float* acc, float p, const float* __restrict__ v_lds) {  // acc += p * v
+__device__ __forceinline__ void axpy4(float* acc, float p, const float* __restrict__ v_lds) {
     if constexpr (N % 4 == 0) {
         const float4* v4 = reinterpret_cast<const float4*>(v_lds);
+        const f32x2 pp = {p, p};
 #pragma unroll
         for (int k = 0; k < N / 4; k++) {
             const float4 v = v4[k];
-            acc[4 * k] = fmaf(p, v.x, acc[4 * k]);
-            acc[4 * k + 1] = fmaf(p, v.y, acc[4 * k + 1]);
-            acc[4 * k + 2] = fmaf(p, v.z, acc[4 * k + 2]);
-            acc[4 * k + 3] = fmaf(p, v.w, acc[4 * k + 3]);
+            const f32x2 lo = __builtin_elementwise_fma(pp, f32x2{v.x, v.y}, f32x2{acc[4 * k], acc[4 * k + 1]});
+            const f32x2 hi = __builtin_elementwise_fma(pp, f32x2{v.z, v.w}, f32x2{acc[4 * k + 2], acc[4 * k + 3]});
+            acc[4 * k] = lo.x;
+            acc[4 * k + 1] = lo.y;
+            acc[4 * k + 2] = hi.x;
+            acc[4 * k + 3] = hi.y;
         }
     } else {
         const float2* v2 = reinterpret_cast<const float2*>(v_lds);
@@ -982,6 +987,22 @@ __device__ __forceinline__ void ef2_write(float* partial, const EFAccM& acc) {
     }
 }
 
+// issue priority of the per-sample chain: 1 (default) its MFMA blocks at s_setprio 1, so a wave entering
+// one keeps the SIMD's matrix pipe fed while the co-resident waves' VALU phases fill in (419,430 rows, A/B on
+// one box, 7 rounds: 1,206 -> 1,165 us); 2 the softmax (VALU) block at s_setprio 1 instead (1,189 us); 0 none
+#ifndef FRONT_PRIO
+#define FRONT_PRIO 1
+#endif
+__device__ __forceinline__ void front_prio(int phase) {  // phase 0: MFMA block starts; 1: softmax starts; 2: chain ends
+    if constexpr (FRONT_PRIO == 1) {
+        if (phase == 0) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (FRONT_PRIO == 2) {
+        if (phase == 1) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+}
+
 __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) void k_front_bwd_mfma(const float* __restrict__ ws,
                                                                    const float* __restrict__ x, int ldx, int B,
                                                                    int parity, const float* __restrict__ dh,
@@ -1028,7 +1049,10 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             }
         }
         wave_sync();
-#pragma unroll 1
+#ifndef FRONT_HALF_UNROLL  // 2: both samples' chains in one body (156 VGPRs) measured 1% slower
+#define FRONT_HALF_UNROLL 1
+#endif
+#pragma unroll FRONT_HALF_UNROLL
         for (int half = 0; half < 2; half++) {
             const int slot = 2 * wave + half;
             if (slot >= nrow) break;  // wave-uniform
@@ -1046,6 +1070,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
 #else
             dp_operands(dh, row0 + slot, c16, q4, df, dt);
 #endif
+            front_prio(0);
             // ---- S^T = K Q^T: tiles [J][I]; k = a = q4 + 4 e, three steps over a < 12 (d_k 10: a = 10, 11
             // read the zero pads) ----
             f32x4_t S[2][2];
@@ -1106,6 +1131,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             // of dP^T; padding rows j (k = 0, so S = 0) are kept out of the max and the sum.  exp2 / rcp
             // (~1 ulp) by default; FRONT_MFMA_FAST_SOFTMAX=0 takes the reference's rounding steps (x /
             // sqrt(10), expf, 1 / sum, as k_front_bwd) -- the gradients' distance to fp64 is the same ----
+            front_prio(1);
 #pragma unroll
             for (int I = 0; I < 2; I++) {
                 float mx = -INFINITY;
@@ -1161,6 +1187,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             }
             f32x4_t (&P)[2][2] = S;
             f32x4_t (&dS)[2][2] = dP;
+            front_prio(0);
             wave_sync();  // the QKV words are dead: the transpose buffer
             // T [i][j] (query-major, rows i < 24, pitch kTp): a C tile's four registers g are consecutive j, so a
             // lane stores them as one 16-byte write (P and dS are 0 in the padding rows and columns)
@@ -1215,6 +1242,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 for (int I = 0; I < 2; I++)  // (query rows i >= 24 hold other words: their dQ columns are not kept)
                     dQ[I] = mfma4(ka[s], T[(16 * I + c16) * kTp + i], dQ[I]);
             }
+            front_prio(2);
             wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
 #pragma unroll
             for (int I = 0; I < 2; I++) {  // dq rows a = 4 q4 .. 4 q4 + 3 of token i: one 16-byte write (a = 10, 11

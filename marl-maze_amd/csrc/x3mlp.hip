@@ -1771,8 +1771,12 @@ static bool bres_plan(int prec, int M, int N, int K, int lda, int ldc, bool bits
     if (!nblk) return false;
     if (nblk > 1 && std::min(e_best, tiles - e_best * (nblk - 1)) < 4 && prec != MM_PREC_X2)
         return false;  // A re-read per block: x3 at K = 460 (3 tiles) measured slower
-    // f16 / x2 at K = 460 (blocks re-reading A of 460 columns): the streaming kernel measured faster (f16 0.81x)
-    if (prec != MM_PREC_X3 && nblk > 1 && K > 288) return false;
+    // f16 / x2 at K = 460 (blocks re-reading A of 460 columns): the streaming kernel measured faster (f16
+    // 0.81x; x2, four 4-5-tile blocks: 568 vs 462 us at 419,430 rows -- BRES_X2_WIDE_K=1 builds that form)
+#ifndef BRES_X2_WIDE_K
+#define BRES_X2_WIDE_K 0
+#endif
+    if (prec != MM_PREC_X3 && nblk > 1 && K > 288 && (prec != MM_PREC_X2 || !BRES_X2_WIDE_K)) return false;
     cfg = prec == MM_PREC_X2 ? C_PAIR : (prec == MM_PREC_F16 && ctb > BresCfg<C_NARROW>::CT) ? C_WIDE : C_NARROW;
     pl.nblk = nblk;
     pl.ctb = ctb;
