@@ -4,7 +4,8 @@ builds, median of REPS rounds of 10 launches each (HIP events):
   LIBS=tools/_var/base.so,marl-maze_amd/libmarlmaze.so CASES=... python tools/ab_libs.py
 
 CASES (comma-separated; M = rows, default 419,430):
-  gemm:PREC:FORM:NxK   FORM fwd (bias+ReLU+bits), bwd (through bits + column sums), plain
+  gemm:PREC:FORM:NxK[:ALGO]   FORM fwd (bias+ReLU+bits), bwd (through bits + column sums), plain; ALGO auto
+                       (default) or stream (x3.set_algo)
   wgrad:PREC:NxK       dW = dY^T X
   front:fwd / front:bwd  the fused actor front-end (M samples)
 """
@@ -31,8 +32,16 @@ def load(path):
 def make(c, M, g):
     parts = c.split(":")
     if parts[0] == "gemm":
-        prec, form, shape = parts[1:]
+        prec, form, shape = parts[1:4]
         N, K = (int(v) for v in shape.split("x"))
+        if len(parts) > 4:  # gemm:PREC:FORM:NxK:ALGO -- x3.set_algo (auto / stream) around each call
+            fn, algo = make(":".join(parts[:4]), M, g), parts[4]
+
+            def run():
+                prev = x3.set_algo(algo)
+                fn()
+                x3.set_algo(prev)
+            return run
         a = torch.randn(M, K, device="cuda", generator=g)
         wf = torch.randn(N, K, device="cuda", generator=g) * 0.05
         bias = torch.randn(N, device="cuda", generator=g)
