@@ -1291,8 +1291,17 @@ __global__ __launch_bounds__(kSumCols * kSumClasses) void k_front_sum(const floa
     const int c = threadIdx.x % kSumCols, k = threadIdx.x / kSumCols;
     const int e = blockIdx.x * kSumCols + c;
     double acc = 0.0;
-    if (e < kPartLen)
-        for (int r = k; r < rows; r += kSumClasses) acc += (double)partial[(size_t)r * kPartLen + e];
+    if (e < kPartLen) {  // 8 rows' loads in flight per batch; the additions in row order (as one row at a time)
+        int r = k;
+        for (; r + 7 * kSumClasses < rows; r += 8 * kSumClasses) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) v[i] = partial[(size_t)(r + i * kSumClasses) * kPartLen + e];
+#pragma unroll
+            for (int i = 0; i < 8; i++) acc += (double)v[i];
+        }
+        for (; r < rows; r += kSumClasses) acc += (double)partial[(size_t)r * kPartLen + e];
+    }
     acc_s[k][c] = acc;
     __syncthreads();
     if (k == 0 && e < kPartLen) {
