@@ -41,6 +41,10 @@ MODEL_PATH = "PPO.pth"  # PPO.py:9 (CWD-relative)
 # the captured rollout's critic on a side stream (a parallel branch of the graph): MARLMAZE_ROLLOUT_SIDE=0 keeps
 # it on the main stream (A/B)
 ROLLOUT_SIDE_STREAM = os.environ.get("MARLMAZE_ROLLOUT_SIDE", "1") != "0"
+# the rollout's critic values in ONE launch over all T (+1) steps' observations after the env loop (they depend on
+# the observations only, and the weights do not change during a rollout): no critic launch and no cross-stream
+# hand-off per step.  MARLMAZE_ROLLOUT_CRITIC=step keeps the per-step form (A/B)
+ROLLOUT_BATCHED_CRITIC = os.environ.get("MARLMAZE_ROLLOUT_CRITIC", "batched") != "step"
 
 
 def _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip):
@@ -211,14 +215,15 @@ class PPO:
             act=torch.zeros((T, n, 2, 2), dtype=torch.int8, device=d),
             logp=torch.zeros((T, n), dtype=torch.float32, device=d),
             rowlogp=torch.zeros((T, 2 * n), dtype=torch.float32, device=d),
-            val=torch.zeros((T, n), dtype=torch.float32, device=d),
-            last_val=torch.zeros((n,), dtype=torch.float32, device=d),
+            val_all=torch.zeros((T + 1, n), dtype=torch.float32, device=d),  # [T] values + the bootstrap row
             rew=torch.zeros((T, n), dtype=torch.float32, device=d),
             done=torch.zeros((T, n), dtype=torch.uint8, device=d),
             stats=torch.zeros((T, n, 2), dtype=torch.int32, device=d),
             adv=torch.zeros((T, n), dtype=torch.float32, device=d),
             rtg=torch.zeros((T, n), dtype=torch.float32, device=d),
         )
+        self._bufs["val"] = self._bufs["val_all"][:T]
+        self._bufs["last_val"] = self._bufs["val_all"][T]
         self.venv.reset(obs=self._bufs["obs"][0], masks=self._bufs["masks"][0])
         self._fresh = True
 
@@ -270,14 +275,17 @@ class PPO:
     def _rollout_steps(self, b, n, T, offset_dev=None):
         head_w, head_b = self.actor.heads()
         cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
-        # the critic and the actor read the same observations and nothing of each other: with the rollout
-        # captured (a few thousand mazes, every kernel latency-bound) the critic runs on a side stream beside
-        # the actor -- two branches of the graph
-        side = (self._critic_stream() if (self.graph_rollout and cur is not None and ROLLOUT_SIDE_STREAM)
-                else None)
+        # the critic reads only the observations, which stay in the [T + 1] buffer: by default its values for
+        # every step come from one launch after the loop (ROLLOUT_BATCHED_CRITIC); the per-step form runs it on
+        # a side stream beside the actor when the rollout is captured (two branches of the graph)
+        batched = ROLLOUT_BATCHED_CRITIC and cur is not None
+        side = (self._critic_stream() if (self.graph_rollout and cur is not None and ROLLOUT_SIDE_STREAM
+                                          and not batched) else None)
         for t in range(T):
             obs_t = b["obs"][t]
-            if side is not None:
+            if batched:
+                pass
+            elif side is not None:
                 side.wait_stream(cur)  # obs[t] written by the previous step's env kernel
                 with torch.cuda.stream(side):
                     self.critic.value_into(obs_t, b["val"][t])
@@ -307,8 +315,15 @@ class PPO:
         if side is not None:
             cur.wait_stream(side)  # every value written before the GAE reads them
         last = None
-        if self.bootstrap:
-            b["last_val"].copy_(self.critic(b["obs"][T]).view(n))
+        if batched:  # V(s_0 .. s_T-1) (and V(s_T) for the bootstrap) in one launch
+            rows = T + 1 if self.bootstrap else T
+            self.critic.value_into(b["obs"][:rows].reshape(rows * n, -1), b["val_all"][:rows].reshape(rows * n))
+            last = b["last_val"] if self.bootstrap else None
+        elif self.bootstrap:  # (the per-step values' arithmetic for V(s_T) too)
+            if cur is not None:
+                self.critic.value_into(b["obs"][T], b["last_val"])
+            else:
+                b["last_val"].copy_(self.critic(b["obs"][T]).view(n))
             last = b["last_val"]
         ops.gae(b["rew"], b["val"], b["done"], last_value=last, gamma=self.discount_rate, lam=self.lam,
                 adv=b["adv"], rtg=b["rtg"])

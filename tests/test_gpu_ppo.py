@@ -497,6 +497,31 @@ def test_graph_rollout_equals_eager(n):
     assert ags[1]._graph is not None and ags[0]._sample_offset == ags[1]._sample_offset
 
 
+@pytest.mark.parametrize("bootstrap", [False, True])
+def test_batched_rollout_critic_equals_per_step(bootstrap, monkeypatch):
+    """The rollout's critic values from one launch after the env loop (PPO.ROLLOUT_BATCHED_CRITIC, the
+    default) are bit-identical to the per-step form (one launch per step, before the step's actions): the
+    values depend on the stored observations only and mm_critic_value's arithmetic per row does not depend
+    on the rows launched beside it.  Every other buffer of the batch is identical too."""
+    from marlmaze import PPO as ppo_mod
+
+    cfg = dict(default_size=(6, 6), max_timestep=20, seed_base=11)
+    T, n = 8, 512
+    outs = []
+    for batched in (False, True):
+        monkeypatch.setattr(ppo_mod, "ROLLOUT_BATCHED_CRITIC", batched)
+        ag = _agent(n_envs=n, horizon=T, batch_size=n * T, sample_seed=9, env_config=cfg, bootstrap=bootstrap)
+        res = []
+        for _ in range(3):
+            b = ag.rollout()
+            res.append({k: b[k].clone() for k in ("obs", "act", "logp", "val", "rew", "done", "adv", "rtg")})
+            ag._carry_over()
+        outs.append(res)
+    for it in range(3):
+        for k in outs[0][it]:
+            assert torch.equal(outs[0][it][k], outs[1][it][k]), (bootstrap, it, k)
+
+
 @pytest.mark.parametrize("dtype", ["f32", "f16"])
 def test_fresh_batch_logp_matches_rollout(dtype):
     """Before the first optimizer step, the update's log-probs of a fresh rollout batch equal the rollout's
