@@ -96,9 +96,12 @@ def _front_bwd_grid(B, dev):
     if grid < 1:
         raise _lib.MMError(f"mm_actor_front_bwd_grid failed with status {grid}")
     return grid
-# the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads) or "row1" (one per lane);
-# bit-identical outputs (csrc/actor_front.hip k_front_fwd2 / k_front_fwd)
+# the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads; 16 samples per workgroup, two
+# workgroups per CU) or "row1" (one per lane; 8 samples, three per CU); bit-identical outputs (csrc/actor_front.hip
+# k_front_fwd2 / k_front_fwd).  "auto": row2 up to FRONT_FWD_ROW2_MAX samples (one round of its grid where row1
+# needs two), row1 above
 FRONT_FWD_ALGO = os.environ.get("MARLMAZE_FRONT_FWD", "row1")
+FRONT_FWD_ROW2_MAX = int(os.environ.get("MARLMAZE_FRONT_FWD_ROW2_MAX", "8192"))
 
 
 def _cu_count(dev):
@@ -536,6 +539,12 @@ class Actor(nn.Module):
                       [_grad_of(p) for p in front_params(self.projection, self.attention)])
 
 
+def _front_fwd_algo(B):
+    if FRONT_FWD_ALGO == "auto":
+        return "row2" if B <= FRONT_FWD_ROW2_MAX else "row1"
+    return FRONT_FWD_ALGO
+
+
 def _front_fwd(x, parity, params):
     """The fused front-end forward (no autograd): (workspace, h [B, 460])."""
     from . import _lib
@@ -559,7 +568,7 @@ def _front_fwd(x, parity, params):
     ws = x3.cached_value("front_prep", params, prep)
     h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
     _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
-                                       _lib.FRONT_FWD[FRONT_FWD_ALGO], stream), "mm_actor_front_fwd_ex")
+                                       _lib.FRONT_FWD[_front_fwd_algo(B)], stream), "mm_actor_front_fwd_ex")
     return ws, h
 
 
