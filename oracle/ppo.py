@@ -2,7 +2,8 @@
 
 Restates, on the CPU in fp32:
 
-* ``gae_fp32``            -- ``PPO.get_GAEs`` (PPO.py:193-203), numpy fp32.
+* ``gae_fp32``            -- ``PPO.get_GAEs`` (PPO.py:193-203), numpy fp32;
+  ``gae_bootstrap_fp32`` the same recursion with a bootstrapped open segment.
 * ``OActor`` / ``OCritic`` -- ``networks.py:13-106`` with the reference's
   module/parameter names, init order and the Projection quirk (Q1: every
   feature embedding reads ``x[:, 0:d_i]``, networks.py:59-63).
@@ -49,6 +50,37 @@ def gae_fp32(rew, val, done, gamma=0.99, lam=0.95):
         else:
             boot = f(g * f(val[t + 1]))
             if done[t + 1]:
+                boot = f(boot * f(0.0))
+            delta = f(f(f(rew[t]) + boot) - v)
+        scale = f(0.0) if done[t] else gl
+        adv = f(delta + f(scale * adv))
+        out[t] = adv
+    return out
+
+
+def gae_bootstrap_fp32(rew, val, done, last_val, gamma=0.99, lam=0.95):
+    """One env's fixed-horizon fragment [T] whose last segment may end mid-episode:
+    the recursion of ``gae_fp32`` (PPO.py:193-203) run backwards over the whole
+    fragment, an episode end (done[t]) cutting it as the reference's per-episode
+    call does, and the open last segment bootstrapped with V(s_T) = last_val
+    (delta = r + gamma V(s_T) - V(s_{T-1})).  Inside an episode the next value
+    is zeroed when the next step is the episode's last (the reference's
+    (1 - d[t+1]) factor, PPO.py:200).  No reference counterpart: the reference
+    only ever cuts at episode ends (its last fragment is treated as terminal).
+    Same fp32 operation order as ``gae_fp32`` step for step."""
+    f = np.float32
+    g = f(gamma)
+    gl = f(gamma * lam)
+    L = len(rew)
+    out = np.zeros(L, np.float32)
+    adv = f(0.0)
+    for t in range(L - 1, -1, -1):
+        v = f(val[t])
+        if done[t]:
+            delta = f(f(rew[t]) - v)
+        else:
+            boot = f(g * f(last_val)) if t + 1 == L else f(g * f(val[t + 1]))
+            if t + 1 < L and done[t + 1]:
                 boot = f(boot * f(0.0))
             delta = f(f(f(rew[t]) + boot) - v)
         scale = f(0.0) if done[t] else gl

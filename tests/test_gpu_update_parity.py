@@ -35,7 +35,8 @@ gradients run; the fixture's 256 rows take neither), every minibatch of the
 reference's recorded train() epoch with the oracle's parameters and Adam state
 teacher-forced in before each step, and BASELINE configs[1] (4,096 mazes,
 T=32: rollout replayed in the oracle on a column subset, then one
-26,214-sample minibatch update).
+26,214-sample minibatch update), and the bench's own loop (horizon 16,
+bootstrap=True: values, bootstrapped advantages and one minibatch update).
 """
 import copy
 
@@ -328,6 +329,68 @@ def test_config1_rollout_and_update_4096_mazes(golden):
     # rollout actor inputs are the 4 facing one-hots (quirk Q1), so the minibatch's gradient sums
     # collapse onto 4 activation vectors and cancel (see the module doc): held to the default 1e-5
     _step_and_compare(ag, actor, critic, batch, "configs[1]")
+
+
+def test_bench_rollout_bootstrap_and_update(golden):
+    """The bench's loop (bench.py: fixed horizon T=16, bootstrap=True -- the
+    open last segment of every env's fragment is bootstrapped with V(s_T), which
+    the reference never does) at 4,096 of its 65,536 mazes.  Every 16th maze
+    column is replayed in the C oracle (bit-exact obs / masks / rewards / dones);
+    the batched critic values V(s_0 .. s_T), V(s_T) included, against the fp32
+    oracle critic at 1e-5 of max|V|; the advantages bit-exact against
+    oracle.ppo.gae_bootstrap_fp32 on the same values; returns = adv + V; then one
+    minibatch of the update against the oracle at the 1e-5 bar."""
+    n, T = 4096, 16
+    cfg = dict(default_size=(10, 10), max_timestep=1200)
+    ag = _agent(n_envs=n, horizon=T, batch_size=n * T, bootstrap=True, sample_seed=13,
+                env_config=dict(cfg, seed_base=0))
+    assert ag.bootstrap
+    act1 = ag.rollout()["act"].cpu().numpy()
+    ag._carry_over()  # as get_batch: the next fragment starts from the last observation
+    b = ag.rollout()  # the second fragment: episodes carried over from the first, mid-episode starts
+    cols = np.arange(0, n, 16)
+    obs = b["obs"].cpu().numpy()[:, cols]
+    masks = b["masks"].cpu().numpy()[:, cols].astype(bool)
+    act = b["act"].cpu().numpy()[:, cols]
+    R = b["rew"].cpu().numpy()[:, cols]
+    D = b["done"].cpu().numpy()[:, cols].astype(bool)
+    # the oracle env is brought to this fragment's first state by the first fragment's actions
+    ora = OracleEnv(len(cols), seeds=cols.astype(np.uint64), **cfg)
+    oo, om = ora.reset_all()
+    for s in range(T):
+        oo, om, _, _ = ora.step_all(act1[s][cols], auto_reset=True)
+    assert np.array_equal(obs[0], oo) and np.array_equal(masks[0], om)
+    for s in range(T):
+        oo, om, orw, od = ora.step_all(act[s], auto_reset=True)
+        assert np.array_equal(obs[s + 1], oo) and np.array_equal(masks[s + 1], om), s
+        assert np.array_equal(R[s], orw) and np.array_equal(D[s], od), s
+    critic = oppo.OCritic()
+    critic.load_state_dict({k: v.cpu() for k, v in ag.critic.state_dict().items()})
+    V = b["val"].cpu().numpy()[:, cols]
+    LV = b["last_val"].cpu().numpy()[cols]
+    with torch.no_grad():
+        rv = np.stack([critic(torch.as_tensor(obs[s])).view(-1).numpy() for s in range(T + 1)])
+    got = np.concatenate([V, LV[None]])
+    assert np.abs(got - rv).max() <= 1e-5 * np.abs(rv).max(), np.abs(got - rv).max() / np.abs(rv).max()
+    A = b["adv"].cpu().numpy()[:, cols]
+    open_end = 0
+    for c in range(len(cols)):
+        ref = oppo.gae_bootstrap_fp32(list(R[:, c].astype(np.float64)), V[:, c], D[:, c], LV[c])
+        assert np.array_equal(A[:, c], ref), c
+        open_end += not D[-1, c]
+    assert open_end > 0  # the bootstrap branch ran
+    assert torch.equal(b["rtg"], b["adv"] + b["val"])
+    B = n * T
+    adv = b["adv"].reshape(B)
+    rtg = adv + b["val"].reshape(B)
+    adv = (adv - adv.mean()) / (adv.std() + 1e-10)
+    sel = torch.randperm(B, generator=torch.Generator().manual_seed(1))[:B // 5].cuda()
+    batch = (b["obs"][:T].reshape(B, 2, 65)[sel].cpu(), b["act"].reshape(B, 2, 2)[sel].float().cpu(),
+             b["logp"].reshape(B)[sel].cpu(), adv[sel].cpu(), rtg[sel].cpu(),
+             b["masks"][:T].reshape(B, 2, 6)[sel].bool().cpu())
+    actor = oppo.OActor()
+    actor.load_state_dict({k: v.cpu() for k, v in ag.actor.state_dict().items()})
+    _step_and_compare(ag, actor, critic, batch, "bench loop, bootstrap")
 
 
 def test_main_py_hyperparameters_minibatch(golden):

@@ -85,6 +85,28 @@ def test_gae_matches_reference(golden):
         assert np.array_equal(a, g[f"L{i}/adv"].astype(np.float32))
 
 
+def test_gae_bootstrap_restatement_on_reference_episodes(golden):
+    """oracle.ppo.gae_bootstrap_fp32 (the bench's bootstrapped fragments; no
+    reference counterpart) on a fragment made of the reference's recorded
+    episodes back to back: every segment closed by its done flag, so the result
+    is the reference's own per-episode advantages whatever V(s_T) is; with the
+    last episode left open, its advantages move and the earlier ones do not."""
+    g = golden("gae")
+    eps = [(list(g[f"L{i}/rew"]), g[f"L{i}/val"], g[f"L{i}/done"].astype(bool)) for i in range(int(g["n"]))]
+    assert all(d[-1] for _, _, d in eps)
+    rew = sum((r for r, _, _ in eps), [])
+    val = np.concatenate([v for _, v, _ in eps]).astype(np.float32)
+    done = np.concatenate([d for _, _, d in eps])
+    ref = np.concatenate([g[f"L{i}/adv"].astype(np.float32) for i in range(int(g["n"]))])
+    for lv in (0.0, 3.5):
+        assert np.array_equal(oppo.gae_bootstrap_fp32(rew, val, done, lv), ref)
+    opened = done.copy()
+    opened[-1] = False
+    a = oppo.gae_bootstrap_fp32(rew, val, opened, 3.5)
+    n_last = len(eps[-1][0])
+    assert np.array_equal(a[:-n_last], ref[:-n_last]) and not np.array_equal(a[-n_last:], ref[-n_last:])
+
+
 @pytest.fixture()
 def four_threads():
     old = torch.get_num_threads()
