@@ -549,12 +549,14 @@ __global__ __launch_bounds__(256) void k_ppo_loss_bwd(const float* __restrict__ 
 // ---------------------------------------------------------------------------
 // The critic's value, fused (networks.py:87-102 forward, inference only): V = w2 . ReLU(W1 ReLU(W0 x + b0) + b1)
 // + b2 for x [M, K0], hidden widths 64 and 64, in ONE launch on the fp32 MFMA (v_mfma_f32_16x16x4_f32: an exact
-// fmaf chain per output, no operand split).  One wavefront per 16 rows, no LDS staging of the weights: each lane
-// issues ALL its operand loads up front -- its 4 x ceil(K0 / 4) W0 values, 4 x 16 W1 values and ceil(K0 / 4) x
-// values (the weights are L2-resident, 50 KB read by every wave) -- so the launch pays one memory round trip,
-// not one per k-step or per staged element (an LDS-staged form measured 20-40 us at 4,096 rows; the three
-// GEMM launches it replaces ~20 us plus two gaps).  The hidden rows go through 4 KB of LDS into the A-operand
-// layout of layer 1; the value head is a cross-lane dot product in a fixed order.
+// fmaf chain per output, no operand split).  A wavefront owns 16 rows at a time, no LDS staging of the weights:
+// each lane holds its 4 x ceil(K0 / 4) W0 values and 4 x 16 W1 values in registers.  Persistent: one resident
+// wavefront per SIMD loads the weights (50 KB, L2-resident) ONCE and then walks the row tiles blockIdx.x,
+// + gridDim.x, ..., with the next tile's x values loaded while the current tile's MFMAs run.  (The first form,
+// one wavefront per 16-row tile, re-read the 50 KB of weights per tile: 3.5 GB of L2 reads for the rollout's
+// batched 1.1M rows, 1.14 ms.)  The hidden rows go through 4 KB of LDS into the A-operand layout of layer 1; the
+// value head is a cross-lane dot product in a fixed order.  Per row the same operations in the same order as
+// the one-tile form: bit-identical values.
 // ---------------------------------------------------------------------------
 constexpr int kCvH = 64;       // hidden width (PPO's Critic: hidden_sizes [64, 64])
 constexpr int kCvMaxK = 132;   // K0 limit (the reference's 2 x 65 observations = 130): 33 k-steps in registers
@@ -563,6 +565,19 @@ constexpr int kCvHp = kCvH + 4;  // LDS row pitch of the hidden rows (64 banks: 
 
 typedef __attribute__((ext_vector_type(4))) float cv_f32x4;
 
+// this lane's x values of row tile `tile` (MFMA 16x16x4 A operand: row c16, k = 4 s + q); zeros past K0, rows past
+// M clamped (computed, never stored), a tile past the last one: zeros (not used)
+__device__ __forceinline__ void cv_load_x(const float* __restrict__ x, int ldx, int K0, int S0, int M, int ntiles,
+                                          int tile, int c16, int q, float (&xa)[kCvMaxS]) {
+    const bool tv = tile < ntiles;
+    const int xr = min(tile * 16 + c16, M - 1);
+#pragma unroll
+    for (int s = 0; s < kCvMaxS; s++) {
+        const int k = 4 * s + q;
+        xa[s] = (tv && s < S0 && k < K0) ? x[(size_t)xr * ldx + k] : 0.f;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_critic_value(const float* __restrict__ x, int ldx, int K0, int M,
                                                      const float* __restrict__ w0, const float* __restrict__ b0,
                                                      const float* __restrict__ w1, const float* __restrict__ b1,
@@ -570,17 +585,15 @@ __global__ __launch_bounds__(64) void k_critic_value(const float* __restrict__ x
                                                      float* __restrict__ v) {
     __shared__ float hs[16 * kCvHp];
     const int lane = threadIdx.x, c16 = lane & 15, q = lane >> 4;
-    const int row0 = blockIdx.x * 16;
     const int S0 = (K0 + 3) >> 2;
-    // operands (MFMA 16x16x4: A = row c16, k = 4 s + q; B = output column c16, same k); out-of-range reads are
-    // zeros (rows past M, columns past K0)
-    const int xr = min(row0 + c16, M - 1);
+    const int ntiles = (M + 15) / 16;
+    int tile = blockIdx.x;
     float xa[kCvMaxS], wa[4][kCvMaxS], wb[4][kCvH / 4];
+    cv_load_x(x, ldx, K0, S0, M, ntiles, tile, c16, q, xa);
 #pragma unroll
     for (int s = 0; s < kCvMaxS; s++) {
         const int k = 4 * s + q;
         const bool ok = s < S0 && k < K0;
-        xa[s] = ok ? x[(size_t)xr * ldx + k] : 0.f;
 #pragma unroll
         for (int t = 0; t < 4; t++) wa[t][s] = ok ? w0[(size_t)(16 * t + c16) * K0 + k] : 0.f;
     }
@@ -588,52 +601,65 @@ __global__ __launch_bounds__(64) void k_critic_value(const float* __restrict__ x
     for (int s = 0; s < kCvH / 4; s++)
 #pragma unroll
         for (int t = 0; t < 4; t++) wb[t][s] = w1[(16 * t + c16) * kCvH + 4 * s + q];
-    // layer 0
-    cv_f32x4 h[4];
+    float bias0[4], bias1[4], wv[4];
 #pragma unroll
-    for (int t = 0; t < 4; t++) h[t] = cv_f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 4; t++) {
+        bias0[t] = b0[16 * t + c16];
+        bias1[t] = b1[16 * t + c16];
+        wv[t] = w2[16 * t + c16];
+    }
+    const float bv = b2[0];
+    for (; tile < ntiles; tile += gridDim.x) {  // wave-uniform
+        // layer 0, with the next tile's x loads in flight
+        cv_f32x4 h[4];
 #pragma unroll
-    for (int s = 0; s < kCvMaxS; s++)
-        if (s < S0) {  // wave-uniform
+        for (int t = 0; t < 4; t++) h[t] = cv_f32x4{0.f, 0.f, 0.f, 0.f};
+        float xn[kCvMaxS];
+        cv_load_x(x, ldx, K0, S0, M, ntiles, tile + gridDim.x, c16, q, xn);
 #pragma unroll
-            for (int t = 0; t < 4; t++) h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[t][s], h[t], 0, 0, 0);
+        for (int s = 0; s < kCvMaxS; s++)
+            if (s < S0) {  // wave-uniform
+#pragma unroll
+                for (int t = 0; t < 4; t++) h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s], wa[t][s], h[t], 0, 0, 0);
+            }
+        // bias + ReLU; lane holds rows 4 q + g, column 16 t + c16 -> LDS, read back as layer 1's A operand
+        __syncthreads();  // the previous tile's layer-1 reads of hs are done
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) hs[(4 * q + g) * kCvHp + 16 * t + c16] = fmaxf(h[t][g] + bias0[t], 0.f);
         }
-    // bias + ReLU; lane holds rows 4 q + g, column 16 t + c16 -> LDS, read back as layer 1's A operand
+        __syncthreads();
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const float bb = b0[16 * t + c16];
+        for (int t = 0; t < 4; t++) h[t] = cv_f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int g = 0; g < 4; g++) hs[(4 * q + g) * kCvHp + 16 * t + c16] = fmaxf(h[t][g] + bb, 0.f);
-    }
-    __syncthreads();
+        for (int s = 0; s < kCvH / 4; s++) {
+            const float a = hs[c16 * kCvHp + 4 * s + q];
 #pragma unroll
-    for (int t = 0; t < 4; t++) h[t] = cv_f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < 4; t++) h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[t][s], h[t], 0, 0, 0);
+        }
+        // value head: V[row] = b2 + sum_j ReLU(h1 + b1)[row][j] w2[j]: this lane's 4 rows x its 4 columns, then
+        // the sum over the 16 lanes sharing the rows -- a fixed order
+        float part[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < kCvH / 4; s++) {
-        const float a = hs[c16 * kCvHp + 4 * s + q];
+        for (int t = 0; t < 4; t++) {
 #pragma unroll
-        for (int t = 0; t < 4; t++) h[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, wb[t][s], h[t], 0, 0, 0);
-    }
-    // value head: V[row] = b2 + sum_j ReLU(h1 + b1)[row][j] w2[j]: this lane's 4 rows x its 4 columns, then the
-    // sum over the 16 lanes sharing the rows -- a fixed order
-    float part[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const float bb = b1[16 * t + c16], ww = w2[16 * t + c16];
-#pragma unroll
-        for (int g = 0; g < 4; g++) part[g] = fmaf(fmaxf(h[t][g] + bb, 0.f), ww, part[g]);
-    }
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) part[g] += __shfl_xor(part[g], o);
-    }
-    if (c16 == 0) {
+            for (int g = 0; g < 4; g++) part[g] = fmaf(fmaxf(h[t][g] + bias1[t], 0.f), wv[t], part[g]);
+        }
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const int r = row0 + 4 * q + g;
-            if (r < M) v[r] = part[g] + b2[0];
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) part[g] += __shfl_xor(part[g], o);
         }
+        if (c16 == 0) {
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int r = tile * 16 + 4 * q + g;
+                if (r < M) v[r] = part[g] + bv;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < kCvMaxS; s++) xa[s] = xn[s];
     }
 }
 
@@ -744,7 +770,23 @@ extern "C" int mm_critic_value(const float* x, int ldx, int K0, int M, int H0, i
         return MM_E_ARG;
     if (H0 != mm::kCvH || H1 != mm::kCvH) return MM_E_ARG;  // the reference critic's [64, 64]
     if (M == 0) return 0;
-    hipLaunchKernelGGL(mm::k_critic_value, dim3((M + 15) / 16), dim3(64), 0, (hipStream_t)stream, x, ldx, K0, M, w0,
-                       b0, w1, b1, w2, b2, v);
+    // persistent: as many one-wavefront workgroups as are resident at once (the occupancy the compiler's register
+    // count allows, times the CUs), or one per row tile when there are fewer tiles
+    static int resident[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return MM_E_ARG;
+    if (!resident[dev]) {
+        int cus = 0, per_cu = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)mm::k_critic_value, 64, 0) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 4;
+        resident[dev] = cus * per_cu;
+    }
+    const int tiles = (M + 15) / 16;
+    const int grid = tiles < resident[dev] ? tiles : resident[dev];
+    hipLaunchKernelGGL(mm::k_critic_value, dim3(grid), dim3(64), 0, (hipStream_t)stream, x, ldx, K0, M, w0, b0, w1,
+                       b1, w2, b2, v);
     return (int)hipGetLastError();
 }

@@ -84,11 +84,12 @@ def test_zero_grad_set_to_none_rebinds_flat_buffer(golden):
         assert np.isfinite(r.cpu().numpy()).all()
 
 
-@pytest.mark.parametrize("M", [1, 63, 4096, 70001])
+@pytest.mark.parametrize("M", [1, 63, 4096, 70001, 17 * 65536 + 5])
 def test_fused_critic_value_matches_oracle(golden, M):
-    """mm_critic_value (the rollout's per-step V, networks.py:87-102) against the fp64 oracle critic: the three
-    layers on the fp32 MFMA in one launch, at 1e-5 of max |V| (ragged row counts: partial 16-row tiles and
-    workgroups)."""
+    """mm_critic_value (the rollout's V, networks.py:87-102) against the fp64 oracle critic: the three layers on
+    the fp32 MFMA in one launch, at 1e-5 of max |V| (ragged row counts: partial 16-row tiles; the bench's batched
+    rollout size, where each persistent wavefront walks many tiles).  Each row's value is independent of the
+    batch it sits in, bit for bit: the same rows permuted, and the first rows alone."""
     from marlmaze.networks import Critic
 
     fx = golden("nets")
@@ -105,3 +106,11 @@ def test_fused_critic_value_matches_oracle(golden, M):
         ref = oc.double()(x.double()).squeeze(-1)
     err = (v.cpu().double() - ref).abs().max().item()
     assert err <= 1e-5 * ref.abs().max().item() + 1e-6, err
+    perm = torch.randperm(M, generator=g)
+    vp = torch.empty(M, device="cuda")
+    cr.value_into(x[perm].cuda(), vp)
+    assert torch.equal(vp.cpu(), v.cpu()[perm])
+    m = min(M, 37)
+    vs = torch.empty(m, device="cuda")
+    cr.value_into(x[:m].cuda(), vs)
+    assert torch.equal(vs, v[:m])
