@@ -80,11 +80,13 @@ def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4, max_st
                 _batch=(steps, batch))
 
 
-def _cpu_epoch_bounded(threads, full_batch, max_steps=1500, updates=1, timeout=60):
+def _cpu_epoch_bounded(threads, full_batch, max_steps=100, updates=1, timeout=90):
     """_cpu_epoch at `threads` threads on a bounded sample, in a child process
     with a time limit (torch at os.cpu_count() threads inside the box's CPU share
     can be very slow on these tiny ops: a run past the limit is reported, not
-    waited for)."""
+    waited for).  The sample is small (100 rollout env-steps, one of the five
+    update passes) because 1,500 steps did not finish in 60 s at 256 threads in
+    a 16-CPU share (round 3 and 4 lines)."""
     import subprocess
     import tempfile
 
