@@ -80,31 +80,83 @@ def _cpu_epoch(threads, batch_size=15000, size=10, max_t=1200, lr=1.4e-4, max_st
                 _batch=(steps, batch))
 
 
-def _cpu_epoch_bounded(threads, full_batch, max_steps=100, updates=1, timeout=90):
-    """_cpu_epoch at `threads` threads on a bounded sample, in a child process
-    with a time limit (torch at os.cpu_count() threads inside the box's CPU share
-    can be very slow on these tiny ops: a run past the limit is reported, not
-    waited for).  The sample is small (100 rollout env-steps, one of the five
-    update passes) because 1,500 steps did not finish in 60 s at 256 threads in
-    a 16-CPU share (round 3 and 4 lines)."""
+_BOUNDED_CHILD = r"""
+import json, sys, time
+t0 = time.time()
+sys.path[:0] = [{repo!r}, {pkg!r}]
+import torch
+from oracle.env import OracleEnv
+from oracle.ppo import CpuPPOPort
+torch.set_num_threads({threads})
+prog = open({prog!r}, "a")
+def log(**k):
+    prog.write(json.dumps(k) + "\n")
+    prog.flush()
+log(stage="start", s=time.time() - t0)
+env = OracleEnv(1, default_size=(10, 10), max_timestep=1200, seeds=[0])
+port = CpuPPOPort(env, batch_size=15000, lr=1.4e-4)
+done, t_roll = 0, 0.0
+while done < {max_steps}:  # the rollout in chunks of 10 env-steps, progress after each
+    t = time.time()
+    steps, _ = port.get_batch(max_steps=10)
+    t_roll += time.time() - t
+    done += steps
+    log(stage="rollout", steps=done, s=t_roll)
+fb = torch.load({fb!r}, weights_only=True)
+t = time.time()
+port.update(tuple(fb["batch"]), updates=1)
+log(stage="update", passes=1, s=time.time() - t)
+"""
+
+
+def _cpu_epoch_bounded(threads, full_batch, max_steps=100, timeout=90):
+    """The train() epoch at `threads` threads on a bounded sample, in a child
+    process with a time limit (torch at os.cpu_count() threads inside the box's
+    CPU share can be very slow on these tiny ops: a run past the limit is
+    reported, not waited for).  The child logs its progress (the rollout in
+    chunks of 10 env-steps, then one of the five update passes on a full epoch's
+    batch), so a run cut by the limit still yields the rollout's rate.  The
+    epoch is extrapolated: full_batch's env-steps at the rollout rate plus five
+    update passes.  (1,500 steps in one piece never finished in 60 s at 256
+    threads in a 16-CPU share, rounds 3-4.)"""
     import subprocess
     import tempfile
 
     with tempfile.TemporaryDirectory() as d:
         fb = os.path.join(d, "batch.pt")
+        prog = os.path.join(d, "progress.jsonl")
         torch.save({"steps": full_batch[0], "batch": list(full_batch[1])}, fb)
-        code = ("import json, sys, torch; sys.path[:0] = [%r, %r]; import bench; "
-                "fb = torch.load(%r, weights_only=True); "
-                "r = bench._cpu_epoch(%d, max_steps=%d, updates=%d, full_batch=(fb['steps'], tuple(fb['batch']))); "
-                "r.pop('_batch'); print(json.dumps(r))") % (REPO, os.path.join(REPO, "marl-maze_amd"), fb, threads,
-                                                             max_steps, updates)
+        code = _BOUNDED_CHILD.format(repo=REPO, pkg=os.path.join(REPO, "marl-maze_amd"), threads=threads, prog=prog,
+                                     max_steps=max_steps, fb=fb)
+        timed_out = False
         try:
-            out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
-            return json.loads(out.stdout.strip().splitlines()[-1])
-        except (subprocess.TimeoutExpired, ValueError, IndexError):
-            return dict(threads=threads, env_steps_per_s=0.0, timed_out_s=timeout,
-                        sampled=f"first {max_steps} rollout env-steps and {updates} of 5 update passes: did not "
-                                f"finish within {timeout} s")
+            subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+        except subprocess.TimeoutExpired:
+            timed_out = True
+        log = []
+        if os.path.exists(prog):
+            with open(prog) as f:
+                log = [json.loads(line) for line in f if line.strip()]
+    roll = [e for e in log if e["stage"] == "rollout"]
+    upd = [e for e in log if e["stage"] == "update"]
+    start = [e["s"] for e in log if e["stage"] == "start"]
+    r = dict(threads=threads, timed_out_s=timeout if timed_out else None,
+             startup_s=start[0] if start else None)
+    if not roll:
+        r.update(env_steps_per_s=0.0, sampled=f"no rollout chunk of 10 env-steps finished within {timeout} s")
+        return r
+    steps, t_roll = roll[-1]["steps"], roll[-1]["s"]
+    r.update(rollout_env_steps_per_s=steps / t_roll)
+    if upd:
+        full = full_batch[0]
+        epoch_s = full * t_roll / steps + 5.0 * upd[-1]["s"]
+        r.update(env_steps=full, epoch_s=epoch_s, rollout_s=full * t_roll / steps, update_s=5.0 * upd[-1]["s"],
+                 env_steps_per_s=full / epoch_s, minibatch=3000, minibatches=25,
+                 sampled=f"first {steps} rollout env-steps and 1 of 5 update passes, extrapolated to the epoch")
+    else:
+        r.update(env_steps_per_s=0.0, sampled=f"{steps} rollout env-steps in {t_roll:.1f} s; the update pass did not "
+                                              f"finish within {timeout} s (rollout rate only)")
+    return r
 
 
 def cpu_baseline():
