@@ -1,6 +1,7 @@
 """The two front-end forward kernels (k_front_fwd: 8 samples per workgroup, three per CU; k_front_fwd2: 16
 samples, two per CU; bit-identical outputs) timed against each other per row count, in one process,
-alternating, median of REPS rounds of 20 launches (HIP events)."""
+alternating, median of REPS rounds of 20 launches (HIP events; at small M the host's launch path dominates
+these, so run it under rocprofv3 --kernel-trace --stats with SIZES=M for the kernels' own times)."""
 import os
 import sys
 
@@ -26,7 +27,9 @@ torch.manual_seed(0)
 actor = Actor([264, 264, 264]).cuda()
 params = front_params(actor.projection, actor.attention)
 reps = int(os.environ.get("REPS", 7))
-for M in (4096, 8192, 12288, 16384, 24576, 52428, 131072, 419430):
+sizes = os.environ.get("SIZES")
+for M in (tuple(int(v) for v in sizes.split(",")) if sizes else (4096, 8192, 12288, 16384, 24576, 52428, 131072,
+                                                                  419430)):
     x = torch.rand(M, 65, device="cuda")
     t = {"row1": [], "row2": []}
     for algo in t:
