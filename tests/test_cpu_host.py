@@ -205,3 +205,22 @@ def test_global_advantage_statistics(world):
     x = torch.randn(1000, dtype=torch.float32)
     m, s = DP.single().global_mean_std(x)
     assert torch.allclose(m, x.mean()) and torch.allclose(s, x.std())
+
+
+def test_bench_bounded_cpu_sample_reports_progress():
+    """bench.py's os.cpu_count()-thread CPU leg (_cpu_epoch_bounded): a finished
+    child extrapolates its rollout chunks and one update pass to the epoch; a
+    child cut by the time limit before any chunk reports that instead of a rate."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from oracle.env import OracleEnv
+    from oracle.ppo import CpuPPOPort
+
+    port = CpuPPOPort(OracleEnv(1, default_size=(10, 10), max_timestep=1200, seeds=[0]), batch_size=15000)
+    steps, batch = port.get_batch(max_steps=40)
+    r = bench._cpu_epoch_bounded(1, (15600, batch), max_steps=20, timeout=120)
+    assert r["timed_out_s"] is None and r["env_steps"] == 15600 and r["env_steps_per_s"] > 0
+    assert r["rollout_env_steps_per_s"] > 0 and r["epoch_s"] > r["update_s"] > 0
+    assert "first 20 rollout env-steps" in r["sampled"]
+    cut = bench._cpu_epoch_bounded(1, (15600, batch), max_steps=20, timeout=0.01)
+    assert cut["timed_out_s"] == 0.01 and cut["env_steps_per_s"] == 0.0
