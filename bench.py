@@ -128,9 +128,11 @@ def _cpu_epoch_bounded(threads, full_batch, max_steps=100, timeout=90):
         torch.save({"steps": full_batch[0], "batch": list(full_batch[1])}, fb)
         code = _BOUNDED_CHILD.format(repo=REPO, pkg=os.path.join(REPO, "marl-maze_amd"), threads=threads, prog=prog,
                                      max_steps=max_steps, fb=fb)
-        timed_out = False
+        timed_out, failed = False, None
         try:
-            subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+            cp = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=timeout)
+            if cp.returncode != 0:  # a crash (import error, OOM kill) is reported as one, not as slowness
+                failed = dict(returncode=cp.returncode, stderr_tail=(cp.stderr or "")[-600:])
         except subprocess.TimeoutExpired:
             timed_out = True
         log = []
@@ -142,7 +144,13 @@ def _cpu_epoch_bounded(threads, full_batch, max_steps=100, timeout=90):
     start = [e["s"] for e in log if e["stage"] == "start"]
     r = dict(threads=threads, timed_out_s=timeout if timed_out else None,
              startup_s=start[0] if start else None)
+    if failed:
+        r.update(error=failed)
     if not roll:
+        if failed:
+            r.update(env_steps_per_s=0.0, sampled=f"the child process failed (exit {failed['returncode']}) before "
+                                                  "a rollout chunk of 10 env-steps finished")
+            return r
         r.update(env_steps_per_s=0.0, sampled=f"no rollout chunk of 10 env-steps finished within {timeout} s")
         return r
     steps, t_roll = roll[-1]["steps"], roll[-1]["s"]
@@ -215,7 +223,9 @@ def main():
     ap.add_argument("--mazes", type=int, default=None,
                     help="mazes per GPU (default 65,536; 32,768 = configs[4]'s 262,144 / 8 with --dtype f16)")
     ap.add_argument("--dtype", choices=("f32", "f16"), default="f32",
-                    help="f32: the GEMMs at fp32-class accuracy (bf16x3 MFMA, the headline); f16: fp16 MFMA operands "
+                    help="f32: the GEMMs at fp32-class accuracy (x2: fp16 hi + lo planes, three fp16 MFMAs per "
+                         "product; a range guard redoes an update at bf16x3 when an operand leaves fp16's range; "
+                         "the headline); f16: fp16 MFMA operands "
                          "with fp32 accumulation and fp32 master weights (BASELINE configs[4])")
     ap.add_argument("--size", type=int, default=10, help="default_size (cells); layout is 2*size-1")
     ap.add_argument("--horizon", type=int, default=16, help="env-steps per maze per iteration")

@@ -307,6 +307,15 @@ int mm_gemm_tp_pack_multi(int prec, const mm_pack_seg_t* segs, int nseg, void* s
 int mm_gemm_wgrad_slices(int prec, int M, int N, int K);
 int mm_gemm_wgrad_partials(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
                            int K, float cscale, float* ws, void* stream);
+/* Range guard of MM_PREC_X2 / MM_PREC_F16 (fp16 planes: |x s| >= 65520 would
+ * round to inf, where the fp32 reference stays finite).  Every kernel that
+ * converts an operand to fp16 planes (mm_gemm_tp_pack(_multi), mm_gemm_nt,
+ * mm_gemm_wgrad(_partials)) ORs bit 0 into a library-wide flag when a value it
+ * converted had |x s| >= 2^15 (or was infinite); its result is then not to be
+ * used -- redo the work at MM_PREC_X3 (fp32's range).
+ * mm_gemm_range_flag: stream-ordered; writes the flag to out[0] (device
+ * memory, may be NULL) and, when clear != 0, resets it. */
+int mm_gemm_range_flag(uint32_t* out, int clear, void* stream);
 
 /* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
  * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),

@@ -67,6 +67,48 @@ struct Prec {
 constexpr float kX2Lo = 2048.f;         // P_X2: lo = RN16(2^11 (x - hi))
 constexpr float kX2LoInv = 1.f / 2048.f;
 
+// Range guard of the fp16-plane precisions.  P_X2 (x s = hi + 2^-11 lo) and P_F16 (x s rounded) hold every
+// operand value as fp16 planes: |x s| >= 65520 rounds hi to inf (lo then to -inf), and every output that
+// value reaches becomes inf or NaN, where the fp32 reference stays finite.  The kernels therefore check
+// their OUTPUT accumulators, not their inputs (cheaper -- an output tile is a few values per lane -- and
+// exact: an out-of-range operand always reaches a non-finite accumulator, an in-range one never does):
+// a lane whose accumulators hold an inf / NaN (exponent field all ones) ORs bit 0 into g_range_flag.  mm_gemm_range_flag reads and clears the flag, stream-ordered,
+// and the caller redoes the work at x3 (bf16x3: fp32's range).  (A non-finite INPUT also raises it: the
+// redo then reproduces fp32's inf / NaN.)  The flag is written by vector atomics only.
+__device__ unsigned int g_range_flag;
+
+template <int P>
+__device__ __forceinline__ void range_acc(uint32_t& rm, const f32x4& a) {  // rm: the largest |bits| (no compares)
+    if constexpr (P != P_X3) {
+#pragma unroll
+        for (int g = 0; g < 4; g++) rm = max(rm, __float_as_uint(a[g]) & 0x7FFFFFFFu);
+    }
+    (void)rm;
+    (void)a;
+}
+// the epilogues' form: a wave-wide mask in SGPRs (v_cmp_class + s_or), no VGPR held over the columns
+template <int P>
+__device__ __forceinline__ void range_val(uint64_t& rb, float x) {
+    if constexpr (P != P_X3) rb |= __builtin_amdgcn_ballot_w64(!__builtin_isfinite(x));
+    (void)rb;
+    (void)x;
+}
+template <int P>
+__device__ __forceinline__ void range_note_wave(uint64_t rb) {
+    if constexpr (P != P_X3) {
+        if (rb != 0 && (threadIdx.x & 63) == 0)
+            __hip_atomic_fetch_or(&g_range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    (void)rb;
+}
+template <int P>
+__device__ __forceinline__ void range_note(uint32_t rm) {
+    if constexpr (P != P_X3) {  // an exponent field of all ones: inf or NaN
+        if (rm >= 0x7F800000u) __hip_atomic_fetch_or(&g_range_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    (void)rm;
+}
+
 constexpr int kBlk = 1536;  // uint16 per (rt, ks) block of P_X3: 3 planes x 512
 constexpr int kRowPad = 256;
 
@@ -320,6 +362,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2v;
 constexpr uint32_t kBufOOB = 0x80000000u;  // an offset past every buffer (num_records < 2^31)
 
+
 // A operand sources.  A wave owns one row tile; per k-step each lane needs the
 // 8 values (row 16 rt + (l & 15), k 32 ks + 8 (l >> 4) .. +7) as three bf16x8.
 struct ASrcTP {  // pre-split TP planes: three lane-linear 1-KiB loads
@@ -460,6 +503,7 @@ enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3 };
 template <int NT, int EM, int P>
 __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int M, int N, int col0, const Epi& ep,
                                              const float* sbias, int lane) {
+    uint64_t rb = 0;  // the range guard (range_val), noted at the end
     const int rq = 4 * (lane >> 4);  // first of this lane's four rows (within the tile)
     const float* sb = sbias + (lane & 15);  // one base register, column c at immediate offset 64 c
     uint32_t bits[kMaskWords] = {0u, 0u, 0u};
@@ -478,6 +522,7 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
         for (int g = 0; g < 4; g++) {
             const int row = 16 * rt + rq + g, bit = 4 * c + g;
             float x = acc[c][g];
+            range_val<P>(rb, x);
             if (Prec<P>::kScaled) x *= ep.cscale;
             if (EM == EM_BWD) {
                 if (!((bits[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
@@ -509,6 +554,7 @@ __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int
 #pragma unroll
         for (int w = 0; w < kMaskWords; w++) mb[w] = bits[w];
     }
+    range_note_wave<P>(rb);
 }
 
 // TP output through a 2-KiB wave-private LDS slice, 32 columns at a time, where
@@ -581,6 +627,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
                                               const Epi& ep, __amdgpu_buffer_rsrc_t crs,
                                               __amdgpu_buffer_rsrc_t srs, const float* sb, int lane) {
     constexpr int NW = (4 * CT + 31) / 32;  // local mask words
+    uint64_t rb = 0;  // the range guard (range_val), noted at the end
     int rq = 4 * (lane >> 4);
     asm volatile("" : "+v"(rq));  // offsets formed here, not hoisted over the main loop and held
     const int row0 = 16 * rt + rq, cl = lane & 15;
@@ -598,11 +645,11 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
         for (int m = 0; m < (CT + 1) / 2; m++)
             if (2 * m < ctn) lbits[m >> 2] |= (uint32_t)mi[m] << (8 * (m & 3));
         if (16 * rt + 16 > M) {  // the last row tile: rows past M masked out (their bits are unspecified)
-            uint32_t rm = 0u;
+            uint32_t rmask = 0u;
 #pragma unroll
-            for (int g = 0; g < 4; g++) rm |= (row0 + g < M ? 1u : 0u) << g;
+            for (int g = 0; g < 4; g++) rmask |= (row0 + g < M ? 1u : 0u) << g;
 #pragma unroll
-            for (int w = 0; w < NW; w++) lbits[w] &= rm * 0x11111111u;
+            for (int w = 0; w < NW; w++) lbits[w] &= rmask * 0x11111111u;
         }
     }
     const float* sbl = sb + cl;
@@ -617,6 +664,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
         for (int g = 0; g < 4; g++) {
             const int bit = 4 * c + g;
             float x = acc[c][g];
+            range_val<P>(rb, x);
             if (Prec<P>::kScaled) x *= ep.cscale;
             if (EM == EM_BWD) {
                 const bool on = (lbits[bit >> 5] >> (bit & 31)) & 1u;
@@ -647,6 +695,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
         for (int m = 0; m < (CT + 1) / 2; m++)
             if (2 * m < ctn) mb[m] = (uint8_t)(lbits[m >> 2] >> (8 * (m & 3)));
     }
+    range_note_wave<P>(rb);
 }
 
 #ifdef X3_STAMPS  // diagnostic builds only (tools/x3_stamps.sh): per-wave phase clocks of k_x3nt
@@ -951,9 +1000,11 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
     }
     float* out = ws + (size_t)s * N * K;
     int tn = tn0, tk = tk0;
+    uint32_t rm = 0;  // the range guard (range_acc)
 #pragma unroll
     for (int u = 0; u < TPW; u++) {
         acc[u] = x2_combine<P>(acc[u], accx[u]);
+        range_acc<P>(rm, acc[u]);  // (tiles past `last` were never accumulated: zeros)
         if (first + u < last) {
             const int col = col0 + 16 * tk + (lane & 15);
 #pragma unroll
@@ -967,6 +1018,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
             tn++;
         }
     }
+    range_note<P>(rm);
 }
 
 // Structured form of k_wgrad for the shapes the actor and critic use (TN, NTK
@@ -1001,11 +1053,19 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     const float* const baseA = dy + (size_t)m_begin * lddy;
     const float* const baseB = x + (size_t)m_begin * ldx + col0;
 
-    // loads through buffer resources over the slice's remaining rows: rows past the slice and columns
-    // past N / K (an out-of-range offset) read zeros -- no per-element branch or 64-bit address (the
-    // exec-masked conditional loads cost ~6 instructions each)
-    int loff[kPer];
+    // loads through one buffer resource per piece slot q over the slice's rows (loop-invariant, built once),
+    // the step's row offset added to the lane's VGPR offset -- no per-element branch or 64-bit address.
+    // EVERY OFFSET IS IN RANGE: lanes whose column is past N / K read the slice's first element (their
+    // values only reach output rows >= N / columns >= K, which are never stored: an MFMA output element
+    // depends on its own A row and B column only), and the rows past the slice in its last, partial step
+    // read it too and are zeroed by a select.  Out-of-range offsets (a load past num_records returns
+    // zeros) made this kernel return zeros in the last quarter-wave (lanes 48-63) of in-range loads of
+    // the same wave in ~3-60% of launches, depending on the form ("The k_wgrad_rect
+    // zeros"; tools/diag_wgrad_capture.py + tools/diag_wgrad_fit.py).  WG_OOB (diagnostic builds) restores
+    // the out-of-range offsets.
+    int loff[kPer], r8q[kPer], ldq[kPer];
     uint32_t voff[kPer];
+    __amdgpu_buffer_rsrc_t rsq[kPer];
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
         const int e = threadIdx.x + kWgThreads * q;
@@ -1013,28 +1073,97 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         const int e2 = isA ? e : e - itemsA, w = isA ? 16 * TN : 16 * NTK;
         const int c = e2 / w, j = e2 - c * w;
         const bool ok = e < items && (isA ? j < N : col0 + j < K);
+#ifdef WG_OOB
         voff[q] = ok ? 4u * (uint32_t)(8 * c * (isA ? lddy : ldx) + j) : kBufOOB;
+#else
+        voff[q] = ok ? 4u * (uint32_t)(8 * c * (isA ? lddy : ldx) + j) : 0u;
+#endif
         loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
-    }
-    float raw[kPer][8];
-    auto load_piece = [&](int q, int r0) {
+        r8q[q] = 8 * c;
         // wave-uniform (itemsA = 64 TN), made scalar: a resource built from a divergent value becomes a
         // readfirstlane waterfall loop per load
-        const bool isA = __builtin_amdgcn_readfirstlane(threadIdx.x + kWgThreads * q) < itemsA;
-        const int ld = isA ? lddy : ldx;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)((isA ? baseA : baseB) + (size_t)r0 * ld), (short)0, (int)((nrows - r0) * ld * 4), 0x00020000);
-        uint32_t o = voff[q];
-        asm volatile("" : "+v"(o));
+        const bool isAu = __builtin_amdgcn_readfirstlane(threadIdx.x + kWgThreads * q) < itemsA;
+        ldq[q] = isAu ? lddy : ldx;
+        rsq[q] = __builtin_amdgcn_make_buffer_rsrc((void*)(isAu ? baseA : baseB), (short)0,
+                                                   (int)(nrows * ldq[q] * 4), 0x00020000);
+    }
+    float raw[kPer][8];
+#ifndef WG_OLDFORM
+    // Every operand register of a staging load stays untouched until that load has completed (DESIGN.md
+    // section 4, "The k_wgrad_rect zeros": a buffer load reads the operands of its last quarter-wave after
+    // the wave has gone on, and a register rewritten in that window -- the compiler reuses a load's address
+    // or offset register as soon as the load has issued -- gave lanes 48-63 zeros).  So: the lane's VGPR
+    // offset ob[q] is advanced IN PLACE one step at a time, just before the next batch (by then the
+    // previous batch has landed: its values were converted and stored); the row strides i ld are scalar
+    // offsets built once; ob, the strides and the resources are held live to the end of the kernel.
+    uint32_t ob[kPer], sri[kPer][8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-#ifdef WG_NO_GLOAD
-            raw[q][i] = o < kBufOOB ? (float)(r0 + i) : 0.f;
-#else
-            raw[q][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, o + 4u * i * ld, 0, 0));
-#endif
+    for (int q = 0; q < kPer; q++) {
+        ob[q] = voff[q];
+#pragma unroll
+        for (int i = 0; i < 8; i++) asm volatile("s_mul_i32 %0, %1, %2" : "=s"(sri[q][i]) : "s"(ldq[q]), "n"(4 * i));
+    }
+    auto hold_operands = [&]() {
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            asm volatile("" ::"v"(ob[q]), "s"(rsq[q]));
+#pragma unroll
+            for (int i = 0; i < 8; i++) asm volatile("" ::"s"(sri[q][i]));
         }
     };
+    auto load_piece = [&](int q, int r0) {  // rows r0 + 8c .. + 7 of the slice; r0 = 0, 32, 64, .. in turn
+        const int ld = ldq[q];
+        if (r0 > 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[q]) : "s"(128 * ld));
+        }
+        if (r0 + 32 <= nrows) {  // a whole step inside the slice (wave-uniform)
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#ifdef WG_NO_GLOAD  // diagnostic builds only: no global loads
+                raw[q][i] = (float)(r0 + i);
+#else
+                raw[q][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsq[q], ob[q], sri[q][i], 0));
+#endif
+            }
+        } else {  // the slice's last, partial step: rows past the slice read its first element, zeroed; these
+                  // loads' offsets are temporaries, so they are waited for here (once per slice at most)
+            const int lim = nrows - r0 - r8q[q];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const float v = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(rsq[q], i < lim ? ob[q] + 4u * i * ld : 0u, 0, 0));
+                raw[q][i] = i < lim ? v : 0.f;
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+    };
+#else  // diagnostic builds: the round-4 form (offsets recomputed per batch, registers reused by the compiler)
+    auto hold_operands = [&]() {};
+    auto load_piece = [&](int q, int r0) {  // rows r0 + 8c .. + 7 of the slice
+        const int ld = ldq[q];
+        uint32_t o = voff[q] + 4u * (uint32_t)(r0 * ld);
+        asm volatile("" : "+v"(o));
+        if (r0 + 32 <= nrows) {  // a whole step inside the slice (wave-uniform)
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+#ifdef WG_NO_GLOAD  // diagnostic builds only: no global loads
+                raw[q][i] = (float)(r0 + i);
+#else
+                raw[q][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsq[q], o + 4u * i * ld, 0, 0));
+#endif
+            }
+        } else {  // the slice's last, partial step: rows past the slice read its first element, zeroed
+            const int lim = nrows - r0 - r8q[q];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const float v =
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsq[q], i < lim ? o + 4u * i * ld : 0u, 0, 0));
+                raw[q][i] = i < lim ? v : 0.f;
+            }
+        }
+    };
+#endif
     auto store_piece_q = [&](int q, uint16_t* dst_set) {
         if (threadIdx.x + kWgThreads * q < items) {
             const bool isA = threadIdx.x + kWgThreads * q < itemsA;
@@ -1061,10 +1190,17 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     for (int q = 0; q < kPer; q++) load_piece(q, 0);
 #pragma unroll
     for (int q = 0; q < kPer; q++) store_piece_q(q, img);
+#ifndef WG_LATE_LOAD
     if (nsteps > 1) {
+#ifdef WG_LGKM0
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+        __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
         for (int q = 0; q < kPer; q++) load_piece(q, 32);
     }
+#endif
     lds_barrier();
     // conversion of the next step's pieces: piece q at slot q * kEvery of the tile loop (VALU beside the
     // MFMAs), the rest after it
@@ -1084,6 +1220,12 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         auto conv_at = [&](int slot) {
             if (kDone > 0 && more && slot % kEvery == 0 && slot / kEvery < kPer) store_piece_q(slot / kEvery, nxt);
         };
+#ifdef WG_LATE_LOAD  // diagnostic builds: the next step's loads issued after the barrier (none in flight across it)
+        if (more) {
+#pragma unroll
+            for (int q = 0; q < kPer; q++) load_piece(q, 32 * (st + 1));
+        }
+#endif
 #ifndef WG_NO_MFMA
         if constexpr (RN > 0) {
             bf16x8 a[RN][3], b[2][3];
@@ -1114,15 +1256,31 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         if (more) {
 #pragma unroll
             for (int q = kDone; q < kPer; q++) store_piece_q(q, nxt);
+#ifndef WG_LATE_LOAD
             if (st + 2 < nsteps) {
+#ifdef WG_LGKM0  // diagnostic builds: this wave's LDS writes completed before the loads issue
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
+                __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
                 for (int q = 0; q < kPer; q++) load_piece(q, 32 * (st + 2));
             }
+#endif
         }
+#ifdef WG_DRAIN  // diagnostic builds: every load landed before the barrier
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkmcnt / expcnt untouched
+#endif
         lds_barrier();
     }
+    hold_operands();
+    uint32_t rm = 0;  // the range guard (range_acc; the clamped duplicate leftover tiles included: same data)
 #pragma unroll
-    for (int u = 0; u < RN * NTK + EX; u++) acc[u] = x2_combine<P>(acc[u], accx[u]);
+    for (int u = 0; u < RN * NTK + EX; u++) {
+        acc[u] = x2_combine<P>(acc[u], accx[u]);
+        range_acc<P>(rm, acc[u]);
+    }
+    range_note<P>(rm);
     float* out = ws + (size_t)s * N * K;
     auto put = [&](const f32x4& v, int tn, int tk) {
         const int col = col0 + 16 * tk + (lane & 15);
@@ -1989,6 +2147,19 @@ static WgPlan wg_plan(int prec, int M, int N, int K) {
     return p;
 }
 
+__global__ void k_range_flag(uint32_t* out, int clear) {
+    if (threadIdx.x == 0) {  // vector atomics on the flag (no scalar-cache writes)
+        const uint32_t v = clear ? __hip_atomic_exchange(&g_range_flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : __hip_atomic_load(&g_range_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (out) out[0] = v;
+    }
+}
+
+extern "C" int mm_gemm_range_flag(uint32_t* out, int clear, void* stream) {
+    hipLaunchKernelGGL(k_range_flag, dim3(1), dim3(64), 0, (hipStream_t)stream, out, clear);
+    return (int)hipGetLastError();
+}
+
 extern "C" long mm_gemm_wgrad_ws_len(int M, int N, int K) {
     if (M <= 0 || N <= 0 || K <= 0) return 0;
     long n = 0;  // the larger of the two precisions' plans
@@ -2048,11 +2219,6 @@ static int launch_rect_p(const WgPlan& p, const float* dy, int lddy, float dscal
                          int N, int K, float cscale, float* ws, hipStream_t s) {
 #define MM_WR(a, b) \
     if (p.TN == a && p.NTK == b) return launch_rect_t<P, a, b>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
-    // x2 at TN = 1, NTK = 17 (the heads' shape, which the update runs at x3): the structured kernel gave a wrong
-    // 16-column tile or row slice in ~1 of 30 launches of 40,000 x 6 x 264 (tools/diag_wgrad_race*.py; every
-    // other precision and the update's x2 shapes ran clean over 40-150 launches each), so this one shape takes
-    // the generic kernel
-    if (P == P_X2 && p.TN == 1 && p.NTK == 17) return 1;
     MM_WR(17, 9) MM_WR(17, 8) MM_WR(1, 17) MM_WR(4, 9) MM_WR(4, 4) MM_WR(1, 4)
 #undef MM_WR
     return 1;

@@ -28,6 +28,7 @@ or treated as an episode end exactly like the reference's last step
 import math
 import os
 import random
+import warnings
 
 import numpy as np
 import torch
@@ -181,6 +182,8 @@ class PPO:
         # host-bound, a replay is one launch
         self.graph_rollout = bool(graph_rollout)
         self._graph = None
+        self.range_redos = 0  # updates redone at x3 by the range guard (_range_guarded)
+        self.range_switched = False  # the rollout's operands left the fp16 range: the networks now run x3
         self._graph_key = None
         self._graph_warm = False
         self._ctr = None  # device base of the sampler's Philox offset in graph replays
@@ -401,7 +404,9 @@ class PPO:
                 ch["obs"][0].copy_(obs0)
                 ch["masks"][0].copy_(masks0)
                 for t in range(C):
-                    ch["val"][t] = self.critic(ch["obs"][t]).view(n)
+                    # the fixed-horizon rollout's value arithmetic (value_into: the fused fp32 kernel), so a
+                    # network's stored values do not depend on the batch mode
+                    self.critic.value_into(ch["obs"][t], ch["val"][t])
                     h = self.actor.trunk(ch["obs"][t].view(2 * n, 65))
                     ops.head_sample(h, head_w, head_b, ch["masks"][t].view(2 * n, 6), self.sample_seed,
                                     self._sample_offset, actions=ch["act"][t].view(2 * n, 2), logp=ch["rowlogp"][t],
@@ -594,20 +599,72 @@ class PPO:
             p_act = p_act.to(torch.int8)
             p_masks = _u8(p_masks)
         K = self.updates_per_batch * len(starts)
-        hist = torch.empty((K, 4), dtype=torch.float32, device=b_obs.device)
-        k = 0
-        for _ in range(self.updates_per_batch):
-            self.decay_lr()
-            for start in starts:
-                sl = slice(start, start + mb)
-                row = self.minibatch_step(p_obs[sl], p_act[sl], p_logp[sl], p_advs[sl], p_rtgs[sl], p_masks[sl],
-                                          **({"out": hist[k]} if self.flat is not None else {}))
-                if self.flat is None:
-                    hist[k] = torch.stack(row)
-                k += 1
-        if self.dp.active:  # local losses -> global-minibatch losses (equal shards); norms are already global
-            self.dp.allreduce_sum(hist)
-            hist /= self.dp.world
+        mbs = [(p_obs[s:s + mb], p_act[s:s + mb], p_logp[s:s + mb], p_advs[s:s + mb], p_rtgs[s:s + mb],
+                p_masks[s:s + mb]) for s in starts]
+
+        def passes():
+            hist = torch.empty((K, 4), dtype=torch.float32, device=b_obs.device)
+            k = 0
+            for _ in range(self.updates_per_batch):
+                self.decay_lr()
+                for args in mbs:
+                    row = self.minibatch_step(*args, **({"out": hist[k]} if self.flat is not None else {}))
+                    if self.flat is None:
+                        hist[k] = torch.stack(row)
+                    k += 1
+            if self.dp.active:  # local losses -> global-minibatch losses (equal shards); norms are already global
+                self.dp.allreduce_sum(hist)
+                hist /= self.dp.world
+            return hist
+
+        if self.flat is None or self.gemm_prec == "x3":
+            return passes()
+        return self._range_guarded(passes)
+
+    # ---- range guard of the fp16-plane GEMMs (x2, f16) ----
+    def set_gemm_prec(self, prec):
+        """The precision of both networks' GEMMs on the GPU ("x2", "x3" or "f16")."""
+        assert prec in networks.GEMM_PRECISIONS
+        self.gemm_prec = self.actor.gemm_prec = self.critic.gemm_prec = prec
+        self._graph = None  # a captured rollout holds the old precision's kernels
+
+    def _range_guarded(self, passes):
+        """Run the update passes; if any GEMM operand they converted to fp16 planes had |x s| >= 2^15 (the
+        library's range flag, mm_gemm_range_flag), restore the parameters and optimizer state and run the
+        same passes again with the bf16x3 GEMMs (fp32's range).  A flag raised before the update (the
+        rollout's forward GEMMs) switches both networks to x3 from now on.  One host synchronisation per
+        update (the flags' read)."""
+        pre = x3.range_flag(clear=True)  # the rollout's conversions since the last update
+        flat = self.flat
+        opts = (self.actor_optim, self.critic_optim)
+        moments = {id(t): t for o in opts for t in (o.exp_avg, o.exp_avg_sq)}
+        snap = (flat.data.clone(), {k: t.clone() for k, t in moments.items()}, [o.t for o in opts],
+                [[g["lr"] for g in o.param_groups] for o in opts])
+        hist = passes()
+        post = x3.range_flag(clear=True)
+        pre_set, post_set = (int(v) for v in torch.cat([pre, post]).tolist())  # the synchronisation
+        if post_set:
+            with torch.no_grad():
+                flat.data.copy_(snap[0])
+                for k, t in moments.items():
+                    t.copy_(snap[1][k])
+            for o, t, lrs in zip(opts, snap[2], snap[3]):
+                o.t = t
+                for g, lr in zip(o.param_groups, lrs):
+                    g["lr"] = lr
+            x3.invalidate_packs()
+            prec = self.gemm_prec
+            self.set_gemm_prec("x3")
+            try:
+                hist = passes()
+            finally:
+                self.set_gemm_prec(prec)
+            self.range_redos += 1
+        if pre_set:
+            warnings.warn(f"marlmaze: a {self.gemm_prec} GEMM operand of the rollout reached |x| >= 2^15 (fp16 "
+                          "planes); both networks run their GEMMs at x3 (bf16x3, fp32 range) from now on")
+            self.set_gemm_prec("x3")
+            self.range_switched = True
         return hist
 
     def train(self):

@@ -43,8 +43,9 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
            "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
-           "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi", "mm_critic_value")
-VERSION = 303  # mm_version() this binding is written for
+           "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi", "mm_critic_value",
+           "mm_gemm_range_flag")
+VERSION = 304  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16, PREC_X2 = 0, 1, 2  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
@@ -195,6 +196,8 @@ def lib():
         L.mm_gemm_wgrad_slices.restype = i32
         L.mm_gemm_wgrad_partials.argtypes = [i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P]
         L.mm_gemm_wgrad_partials.restype = i32
+        L.mm_gemm_range_flag.argtypes = [P, i32, P]
+        L.mm_gemm_range_flag.restype = i32
         L.mm_colsum_multi_ws_len.argtypes = [ctypes.POINTER(ColsumSeg), i32]
         L.mm_colsum_multi_ws_len.restype = ctypes.c_long
         L.mm_colsum_multi.argtypes = [ctypes.POINTER(ColsumSeg), i32, P, P]

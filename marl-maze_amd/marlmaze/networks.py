@@ -651,13 +651,14 @@ class Critic(nn.Module):
         copy (GPU engine shapes only)."""
         from . import _lib
 
-        x = x.reshape(x.shape[0], -1)
+        x = x.reshape(-1, self.agent_amount * OBS_SPACE)  # as forward(): a mismatched input fails here
         if not self._engine(x):
             out.copy_(self(x).reshape(out.shape))
             return out
         w0, b0, w1, b1, w2, b2 = self._params()
-        if (len(self.layers) == 3 and w0.shape[0] == 64 and w1.shape == (64, 64) and w2.shape == (1, 64)
-                and x.shape[1] <= 132 and out.is_contiguous()):
+        # the kernel takes x's width as w0's row stride: the fused path only where they agree
+        if (len(self.layers) == 3 and w0.shape[0] == 64 and w0.shape[1] == x.shape[1] and w1.shape == (64, 64)
+                and w2.shape == (1, 64) and x.shape[1] <= 132 and out.is_contiguous()):
             # the three layers in one launch on the fp32 MFMA (mm_critic_value; also for the fp16 networks: the
             # rollout's values are then fp32-class, the update's critic runs in fp16)
             _lib.check(_lib.lib().mm_critic_value(_lib.ptr(x), x.stride(0), x.shape[1], x.shape[0], 64, 64,

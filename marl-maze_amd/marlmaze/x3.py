@@ -15,10 +15,11 @@ PRECS = {"x3": _lib.PREC_X3, "f16": _lib.PREC_F16, "x2": _lib.PREC_X2}
 
 
 class TP:
-    __slots__ = ("buf", "R", "C", "prec")
+    __slots__ = ("buf", "R", "C", "prec", "src")
 
     def __init__(self, R, C, device, buf=None, prec="x3"):
         self.R, self.C, self.prec = int(R), int(C), prec
+        self.src = None  # (fp32 tensor, trans) it was packed from: gemm(checked=True) repacks it at x3
         n = _lib.lib().mm_gemm_tp_len(PRECS[prec], self.R, self.C)
         self.buf = buf if buf is not None else torch.empty(n, dtype=torch.int16, device=device)
         assert self.buf.numel() >= n
@@ -115,6 +116,7 @@ def pack(x, out=None, trans=False, prec="x3"):
     assert (res.R, res.C, res.prec) == (R, C, prec)
     _lib.check(_lib.lib().mm_gemm_tp_pack(PRECS[prec], _lib.ptr(x), R, C, x.stride(0), int(trans), res.ptr(),
                                           _lib.stream_ptr()), "mm_gemm_tp_pack")
+    res.src = (x, bool(trans))
     if cache:
         _cache_put(x, key, res)
     return res
@@ -184,12 +186,23 @@ class deferred:
         self.cols, self.sums, self.keep = [], [], []
 
 
-def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None, ascale=1.0, out=None):
+def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None, ascale=1.0, out=None,
+         checked=False):
     """out = (1/ascale) ((ascale A) B^T) (+bias)(ReLU) in B's precision (mm_gemm_nt):
     A fp32 [M, K] row-major (16-byte rows, or 8-byte rows for N <= 64), B = TP
     [N, K].  mbits_out records the ReLU mask; mbits_in applies one (the input
     gradient through the ReLU below) with colsum its per-tile column sums.
-    ascale: a power of two for fp16 operands (1 for x3)."""
+    ascale: a power of two for fp16 operands (1 for x3).
+    checked (x2 / f16): read the range flag after the call (a synchronisation) and, when an operand left
+    the fp16 range, redo the GEMM at x3 from B's source tensor (pack() records it)."""
+    if checked and b.prec != "x3":
+        assert b.src is not None, "checked=True needs a TP made by pack()"
+        range_flag(clear=True)
+        res = gemm(a, b, bias, relu, mbits_in, mbits_out, colsum, ascale, out)
+        if int(range_flag(clear=True).item()):
+            src, trans = b.src
+            res = gemm(a, pack(src, trans=trans, prec="x3"), bias, relu, mbits_in, mbits_out, colsum, 1.0, out)
+        return res
     N, K = b.R, b.C
     assert a.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1 and a.shape[1] == K, (a.shape, K)
     M = a.shape[0]
@@ -202,6 +215,17 @@ def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None
     return out
 
 
+def range_flag(out=None, clear=True):
+    """The library's range flag of the fp16-plane precisions (mm_gemm_range_flag): a device int32 [1],
+    nonzero when an x2 / f16 operand converted since the last clear had |x s| >= 2^15 (its GEMM's result
+    is not to be used: redo it at x3).  Stream-ordered; clears the flag unless clear=False."""
+    if out is None:
+        out = torch.empty(1, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib().mm_gemm_range_flag(_lib.ptr(out), int(bool(clear)), _lib.stream_ptr()),
+               "mm_gemm_range_flag")
+    return out
+
+
 def set_algo(name):
     """The kernel gemm() runs (mm_gemm_nt_algo, process-wide): "auto" = B resident in LDS where the
     shape fits, "stream" = B streamed per k-step.  Returns the previous setting's name."""
@@ -209,11 +233,18 @@ def set_algo(name):
     return {v: k for k, v in _lib.GEMM_ALGO.items()}[prev]
 
 
-def wgrad(dy, x, prec="x3", dscale=1.0, out=None):
+def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
     """dW [N, K] = dY^T X summed over the M rows (mm_gemm_wgrad), dY [M, N] and
     X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two).
     Inside a ``deferred()`` scope with ``out`` given, the row-slice partials'
-    sum runs when the scope ends."""
+    sum runs when the scope ends.  checked (x2 / f16): as gemm()'s -- redone at
+    x3 when an operand left the fp16 range."""
+    if checked and prec != "x3":
+        range_flag(clear=True)
+        res = wgrad(dy, x, prec, dscale, out)
+        if int(range_flag(clear=True).item()):
+            res = wgrad(dy, x, "x3", 1.0, out)
+        return res
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dy.stride(1) == 1 and x.stride(1) == 1

@@ -170,3 +170,34 @@ def test_gemm_row_chunks(algo):
     ref = (dy[rows].double() @ w2.double()) * (y[rows] > 0)
     assert _rel_err(dx[rows], ref, dy[rows].double().abs() @ w2.double().abs()) < TOL["x3"]
     assert torch.allclose(cs.double().sum(0), dx.double().sum(0), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(40000, 264, 264), (40000, 264, 460), (3000, 64, 130)])
+def test_x2_range_guard(M, N, K):
+    """Operands beyond fp16's range (|x s| >= 2^16: hi would round to inf, the product to inf / NaN where
+    fp32 stays finite): the x2 kernels raise the library's range flag (mm_gemm_range_flag), and the checked
+    forms redo the GEMM at x3 -- forward, scaled input gradient and weight gradient at the fp32-class bar.
+    In-range operands never raise it."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    x3.range_flag(clear=True)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) * 0.05
+    x3.gemm(a, x3.pack(w, prec="x2"))
+    assert int(x3.range_flag().item()) == 0  # in range: no flag
+    big = a * 2.0**17  # activations beyond 2^16
+    ref = big.double() @ w.double().t()
+    scale = big.double().abs() @ w.double().abs().t()
+    y = x3.gemm(big, x3.pack(w, prec="x2"))
+    assert int(x3.range_flag().item()) == 1 and not torch.isfinite(y).all()  # detected (not silent)
+    y = x3.gemm(big, x3.pack(w, prec="x2"), checked=True)
+    assert torch.isfinite(y).all() and _rel_err(y, ref, scale) < TOL["x2"]
+    # the input-gradient form: dY of a mean over M rows scaled by 2^floor(log2 M), here beyond 2^16 after it
+    dy = torch.randn(M, N, device="cuda", generator=g) * 4.0
+    s = float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
+    dx = x3.gemm(dy, x3.pack(w, trans=True, prec="x2"), ascale=s, checked=True)
+    assert _rel_err(dx, dy.double() @ w.double(), dy.double().abs() @ w.double().abs()) < TOL["x2"]
+    # the weight gradient: X beyond 2^16, and dY whose scaled values are
+    dw = x3.wgrad(dy, big, prec="x2", dscale=s, checked=True)
+    refw = dy.double().t() @ big.double()
+    assert _rel_err(dw, refw, dy.double().abs().t() @ big.double().abs()) < TOL["x2"]
+    assert int(x3.range_flag().item()) == 0  # the checked forms leave the flag clear

@@ -475,3 +475,46 @@ def test_update_calls_no_library_gemm(golden, monkeypatch):
     ag.rollout()
     ag.minibatch_step(*batch)
     torch.cuda.synchronize()
+
+
+def test_update_range_guard_redoes_at_x3(golden):
+    """The update's range guard (PPO._range_guarded): with the trunk's and the critic's first-layer weights
+    scaled so that the hidden activations exceed fp16's range (2^16), the x2 update raises the library's
+    range flag, and the update is redone from the snapshot at x3 -- its parameters, Adam moments and step
+    counts then equal, bit for bit, those of the same update run at x3 from the start, and are finite.
+    An in-range update is not redone and equals the unguarded x2 passes bit for bit."""
+    fx = golden("nets")
+    actor, critic = _oracle_nets(fx)
+    with torch.no_grad():
+        actor.layers[0].weight.mul_(2.0 ** 17)
+        critic.layers[0].weight.mul_(2.0 ** 17)
+    S = 4096
+    obs, act, old, adv, rtg, masks = (t.cuda() for t in _minibatch(fx, S, noise=0.05))
+    vals = rtg - adv
+
+    from marlmaze import x3
+
+    def run(prec):
+        x3.range_flag(clear=True)  # (no flag left over from an earlier test)
+        ag = _agent(n_envs=64, sample_seed=7)
+        _to_gpu(ag, actor, critic)
+        ag.set_gemm_prec(prec)
+        ag.update(obs, act, old, masks, adv, vals, index_list=torch.arange(S))
+        torch.cuda.synchronize()
+        return ag
+
+    guarded, plain = run("x2"), run("x3")
+    assert guarded.range_redos == 1 and plain.range_redos == 0
+    assert guarded.gemm_prec == "x2"  # the networks stay on x2 after the redo
+    assert torch.isfinite(guarded.flat.data).all()
+    assert torch.equal(guarded.flat.data, plain.flat.data)
+    assert torch.equal(guarded.actor_optim.exp_avg, plain.actor_optim.exp_avg)
+    assert torch.equal(guarded.actor_optim.exp_avg_sq, plain.actor_optim.exp_avg_sq)
+    assert guarded.actor_optim.t == plain.actor_optim.t == 25
+    # in range: no redo, and the same arithmetic as the update without the guard
+    actor2, critic2 = _oracle_nets(fx)
+    x3.range_flag(clear=True)
+    ag = _agent(n_envs=64, sample_seed=7)
+    _to_gpu(ag, actor2, critic2)
+    ag.update(obs, act, old, masks, adv, vals, index_list=torch.arange(S))
+    assert ag.range_redos == 0 and ag.gemm_prec == "x2" and torch.isfinite(ag.flat.data).all()
