@@ -1,75 +1,58 @@
 """Offline (CPU) analysis of the wrong weight-gradient partials captured by tools/diag_wgrad_capture.py:
-for every bad (run, slice), which output elements are wrong, and which per-step / per-8-row-chunk
-contributions of the kernel's own arithmetic explain the error (least squares per 16-column tile).
+every wrong (run, slice) partial is fit, by least squares, as a sum of single staging loads that returned
+zero -- one load = one row m of the slice (step m // 32, chunk (m % 32) // 8, row i = m % 8) over one
+16-lane group of columns (a B k-tile) or over the dY columns (A).  A residual ~1e-6 of the error means the
+partial is explained exactly.  Used for DESIGN.md section 4, "The k_wgrad_rect zeros".
 
-  python tools/diag_wgrad_fit.py gpurun_out/r05/capture_x2_40000x6x264.npz
+  python tools/diag_wgrad_fit.py gpurun_out/r05/capture_wg_soff2.npz [N_SHOW]
 """
 import sys
 
 import numpy as np
 
 
-def x2_split(v, s):
-    """The kernel's P_X2 operand split: hi = RN16(v s), lo = RN16(2^11 (v s - hi))."""
-    vs = (v.astype(np.float32) * np.float32(s)).astype(np.float32)
-    hi = vs.astype(np.float16).astype(np.float32)
-    lo = ((vs - hi) * np.float32(2048)).astype(np.float16).astype(np.float32)
-    return hi.astype(np.float64), lo.astype(np.float64)
-
-
-def main(path):
+def main(path, nshow=12):
     z = np.load(path)
-    N, K, rows, s = int(z["N"]), int(z["K"]), int(z["rows"]), float(z["dscale"])
+    N, K, rows = int(z["N"]), int(z["K"]), int(z["rows"])
     slices = list(z["slices"])
-    print(f"{path}: {len(z['bad_run'])} bad partials, slices {slices}, rows per slice {rows}")
-    for b, (run, sl) in enumerate(zip(z["bad_run"], z["bad_slice"])):
-        i = slices.index(sl)
-        dy, x = z["dy_rows"][i], z["x_rows"][i]
-        ah, al = x2_split(dy, s)
-        bh, bl = x2_split(x, 1.0)
-        nst = (rows + 31) // 32
-        # the kernel's contribution of every 8-row chunk: hh part and cross part (x 2^-11), scaled by 1/s
-        chunks_hh = np.stack([ah[8 * c:8 * c + 8].T @ bh[8 * c:8 * c + 8] for c in range(4 * nst)]) / s
-        chunks_x = np.stack([(al[8 * c:8 * c + 8].T @ bh[8 * c:8 * c + 8] + ah[8 * c:8 * c + 8].T @ bl[8 * c:8 * c + 8])
-                             for c in range(4 * nst)]) * (2.0 ** -11) / s
-        model = chunks_hh.sum(0) + chunks_x.sum(0)
+    nst = rows // 32
+    print(f"{path}: {len(z['bad_run'])} bad partials kept, slices {slices}, rows per slice {rows}")
+    for b in range(min(nshow, len(z["bad_run"]))):
+        i = slices.index(z["bad_slice"][b])
+        dy, x = z["dy_rows"][i].astype(np.float64), z["x_rows"][i].astype(np.float64)
         got = z["bad_part"][b].astype(np.float64)
-        err = got - model
-        scale = np.abs(model).max()
-        bad = np.abs(err) > 1e-5 * scale
+        err = got - dy.T @ x
+        bad = np.abs(err) > 1e-5 * np.abs(dy.T @ x).max()
         tiles = sorted(set((np.nonzero(bad.any(0))[0] // 16).tolist()))
-        nrows = sorted(set(np.nonzero(bad.any(1))[0].tolist()))
-        print(f"\nrun {run} slice {sl}: max |err| / max |model| {np.abs(err).max() / scale:.3e}, "
-              f"{bad.sum()} wrong of {N * K}; n rows {nrows[:12]}{'...' if len(nrows) > 12 else ''} "
-              f"({len(nrows)}), k-tiles {tiles}")
-        good_err = np.abs(z['good_part'][i].astype(np.float64) - model).max() / scale
-        print(f"   the first run's partial of this slice vs the model: {good_err:.2e}")
-        for t in tiles[:6]:
-            cols = slice(16 * t, min(K, 16 * t + 16))
-            e = err[:, cols].ravel()
-            # err = sum_j alpha_j * (chunk j contribution), hh and cross parts separately
-            basis = np.concatenate([chunks_hh[:, :, cols].reshape(4 * nst, -1),
-                                    chunks_x[:, :, cols].reshape(4 * nst, -1)])
-            coef, *_ = np.linalg.lstsq(basis.T, e, rcond=None)
-            res = np.abs(basis.T @ coef - e).max() / np.abs(e).max()
-            big = [(("hh" if j < 4 * nst else "x") + f" step {(j % (4 * nst)) // 4} chunk {j % 4}", round(c, 3))
-                   for j, c in enumerate(coef) if abs(c) > 0.05]
-            print(f"   tile {t}: err fit by chunk contributions, residual {res:.3f}: {big[:12]}")
-            # err = (tile t' contribution - tile t contribution) of one step: a fragment of another tile
-            for tp in range(-(-K // 16)):
-                if tp == t:
-                    continue
-                cp = slice(16 * tp, min(K, 16 * tp + 16))
-                if cp.stop - cp.start != cols.stop - cols.start:
-                    continue
-                for st in range(nst):
-                    cand = (chunks_hh[4 * st:4 * st + 4].sum(0) + chunks_x[4 * st:4 * st + 4].sum(0))
-                    d = (cand[:, cp] - cand[:, cols]).ravel()
-                    r = np.abs(d - e).max() / np.abs(e).max()
-                    if r < 0.05:
-                        print(f"   tile {t}: err = step {st}'s B of tile {tp} in place of its own (residual {r:.3f})")
+        out = []
+        if len(tiles) <= 4:  # B loads: per k-tile, which rows of which chunk lost their value
+            for t in tiles:
+                cols = slice(16 * t, 16 * t + 16)
+                e = err[:, cols].ravel()
+                best = None
+                for c in range(4):
+                    ms = [32 * st + 8 * c + r for st in range(nst) for r in range(8)]
+                    basis = np.array([-np.outer(dy[m], x[m, cols]).ravel() for m in ms]).T
+                    coef, *_ = np.linalg.lstsq(basis, e, rcond=None)
+                    res = np.abs(basis @ coef - e).max() / np.abs(e).max()
+                    if best is None or res < best[0]:
+                        best = (res, c, [(ms[k] // 32, ms[k] % 8, round(float(coef[k]), 3))
+                                         for k in np.nonzero(np.abs(coef) > 0.05)[0]])
+                out.append(f"B k-tile {t}: chunk {best[1]}, zeroed (step, row, coef) {best[2]}, residual {best[0]:.1e}")
+        else:  # A loads (dY, all columns): rows of chunk 3 (lanes 48-63 of wave 0)
+            e = err.ravel()
+            best = None
+            for c in range(4):
+                ms = [32 * st + 8 * c + r for st in range(nst) for r in range(8)]
+                basis = np.array([-np.outer(dy[m], x[m]).ravel() for m in ms]).T
+                coef, *_ = np.linalg.lstsq(basis, e, rcond=None)
+                res = np.abs(basis @ coef - e).max() / np.abs(e).max()
+                if best is None or res < best[0]:
+                    best = (res, c, [(ms[k] // 32, ms[k] % 8, round(float(coef[k]), 3))
+                                     for k in np.nonzero(np.abs(coef) > 0.05)[0]])
+            out.append(f"A: chunk {best[1]}, zeroed (step, row, coef) {best[2]}, residual {best[0]:.1e}")
+        print(f"run {z['bad_run'][b]} slice {z['bad_slice'][b]}: " + "; ".join(out))
 
 
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
-        main(p)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 12)
