@@ -821,6 +821,39 @@ static_assert(kTok * kQp <= kMSample && 24 * kTp <= kMSample, "QKV and T live in
 // zeroed words after the last sample's region, so that its padding rows read this kernel's own data (words
 // of another kernel could hold anything, and a huge finite value times the zero weight it gets is not 0)
 constexpr int kMPad = ((32 * kQp > 32 * kTp ? 32 * kQp : 32 * kTp) - kMSample + 3) & ~3;
+// LDS bank swizzles of the per-sample chain (MI355X LDS: ds_read_b32 serves lanes 0-31 and 32-63 in one
+// cycle each when their 32 banks are distinct).  The chain's b32 reads touch 16 rows x 2 k-lanes per group;
+// with row pitches that are multiples of 4 (the float4 writes need them) rows r and r + 8 share banks, and
+// the transposed reads of T (dQ) put 4 lanes on a bank.  So the column index is XORed with a row-dependent
+// value below 4 (a permutation inside each float4: the float4 writes permute their components instead):
+//   QKV, q | k words (< 24): bit 1 flipped on rows with bit 3 set -- the S^T operand reads conflict-free;
+//   T: k ^ L(r), L(r) = (r & 1) | 2 ((r >> 3) & 1) -- the dQ column reads conflict-free.
+// Modelled per access (lane groups and bank rules of MI355X_MICROARCH.md): 108 -> 28 extra LDS cycles per
+// sample over the chain's 156.  Measured (419,430 rows, tools/ab_libs.py, profiles/r05_front_bwd_swizzle.txt):
+// SQ_LDS_BANK_CONFLICT 98.2M -> 64.6M, but the swizzle's selects and XORed addresses add 9% VALU
+// instructions in a kernel bound by issue and dependency waits, not by LDS: 1,151 us plain, 1,166 us q|k
+// only (bit 0), 1,204 us both (bits 0 + 1).  So FRONT_SWZ=0 (plain) is the default; 1 / 2 / 3 select them.
+#ifndef FRONT_SWZ
+#define FRONT_SWZ 0
+#endif
+__device__ __forceinline__ int qk_sw(int r) { return (FRONT_SWZ & 1) ? 2 * ((r >> 3) & 1) : 0; }
+__device__ __forceinline__ int t_sw(int r) { return (FRONT_SWZ & 2) ? ((r & 1) | (((r >> 3) & 1) << 1)) : 0; }
+// the swizzled column c16 of T's row kh_row(s, q4) (L of that row: bit 0 = s's for s < 4, q4's for s >= 4;
+// bit 1 = q4's bit 1 for s < 4, 0 for the rows 16-23)
+__device__ __forceinline__ int t_col(int s, int c16, int q4) {
+    if constexpr ((FRONT_SWZ & 2) == 0) return c16;
+    return s < 4 ? c16 ^ ((s & 1) | (q4 & 2)) : c16 ^ (q4 & 1);
+}
+// a C tile's four registers to words dst[g ^ x] (x < 4): the halves by address (two 8-byte writes), the
+// pairs inside them by select
+__device__ __forceinline__ void t_store(float* dst, const f32x4_t& v, int x) {
+    const bool sw = x & 1;
+    float2* d2 = reinterpret_cast<float2*>(dst);
+    const int h = (x >> 1) & 1;
+    d2[h] = sw ? make_float2(v[1], v[0]) : make_float2(v[0], v[1]);
+    d2[h ^ 1] = sw ? make_float2(v[3], v[2]) : make_float2(v[2], v[3]);
+}
+
 #ifndef FRONT_MFMA_FAST_SOFTMAX  // 1: exp2 / rcp / * (1 / sqrt(10)); 0: the reference's steps (12% slower)
 #define FRONT_MFMA_FAST_SOFTMAX 1
 #endif
@@ -1037,12 +1070,16 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
 #else
                 affine4t<kQkv>(tab + tok * kTabS, tab + tok * kTabS + kQkv * kPin, xv, o);
 #endif
-                q[0] = make_float4(o[0], o[1], o[2], o[3]);
-                q[1] = make_float4(o[4], o[5], o[6], o[7]);
-                q[2] = make_float4(o[8], o[9], 0.f, 0.f);
-                q[3] = make_float4(o[10], o[11], o[12], o[13]);
-                q[4] = make_float4(o[14], o[15], o[16], o[17]);
-                q[5] = make_float4(o[18], o[19], 0.f, 0.f);
+                // q | k: the two halves of each float4 trade places on swizzled rows (see qk_sw): two 8-byte
+                // writes at swapped offsets, no value selects
+                float2* q2 = reinterpret_cast<float2*>(q);
+                const int x = qk_sw(tok) >> 1, y = x ^ 1;
+                q2[0 + x] = make_float2(o[0], o[1]), q2[0 + y] = make_float2(o[2], o[3]);
+                q2[2 + x] = make_float2(o[4], o[5]), q2[2 + y] = make_float2(o[6], o[7]);
+                q2[4 + x] = make_float2(o[8], o[9]), q2[4 + y] = make_float2(0.f, 0.f);
+                q2[6 + x] = make_float2(o[10], o[11]), q2[6 + y] = make_float2(o[12], o[13]);
+                q2[8 + x] = make_float2(o[14], o[15]), q2[8 + y] = make_float2(o[16], o[17]);
+                q2[10 + x] = make_float2(o[18], o[19]), q2[10 + y] = make_float2(0.f, 0.f);
 #pragma unroll
                 for (int c = 0; c < kEmb / 4; c++)
                     q[6 + c] = make_float4(o[20 + 4 * c], o[21 + 4 * c], o[22 + 4 * c], o[23 + 4 * c]);
@@ -1080,8 +1117,9 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 for (int t = 0; t < 2; t++)
 #pragma unroll
                     for (int e = 0; e < 3; e++) {
-                        kf[t][e] = QKV[(16 * t + c16) * kQp + kKO + q4 + 4 * e];
-                        qf[t][e] = QKV[(16 * t + c16) * kQp + kQO + q4 + 4 * e];
+                        const int qx = q4 ^ qk_sw(c16);  // rows 16 t + c16: bit 3 is c16's; (k ^ x) = 4 (k >> 2) + (q4 ^ x)
+                        kf[t][e] = QKV[(16 * t + c16) * kQp + kKO + 4 * e + qx];
+                        qf[t][e] = QKV[(16 * t + c16) * kQp + kQO + 4 * e + qx];
                     }
 #pragma unroll
                 for (int J = 0; J < 2; J++)
@@ -1122,9 +1160,10 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 const int ca = min(c16, kKq);
 #pragma unroll
                 for (int s = 0; s < kKH; s++) {
-                    const int r = kh_row(s, q4);
-                    qb[s] = QKV[r * kQp + kQO + ca];
-                    ka[s] = r < kTok ? QKV[r * kQp + kKO + ca] : 0.f;
+                    // rows kh_row(s, q4): bit 3 is q4's bit 1 for s < 4, 0 for s >= 4 (rows 16-23)
+                    const int r = kh_row(s, q4), cx = s < 4 ? ca ^ qk_sw(4 * q4) : ca;
+                    qb[s] = QKV[r * kQp + kQO + cx];
+                    ka[s] = r < kTok ? QKV[r * kQp + kKO + cx] : 0.f;
                 }
             }
             // ---- softmax over j per query column i, then dS^T = P (dP - rowsum(P dP)) / sqrt(10) in place
@@ -1198,7 +1237,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 if (16 * I + c16 < 24)
 #pragma unroll
                     for (int J = 0; J < 2; J++)
-                        *reinterpret_cast<f32x4_t*>(T + (16 * I + c16) * kTp + 16 * J + 4 * q4) = P[J][I];
+                        t_store(T + (16 * I + c16) * kTp + 16 * J + 4 * q4, P[J][I], t_sw(c16));
             wave_sync();
             f32x4_t dV[2][2];
 #pragma unroll
@@ -1212,7 +1251,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 const int i = kh_row(s, q4);
                 float pa[2];
 #pragma unroll
-                for (int J = 0; J < 2; J++) pa[J] = T[i * kTp + 16 * J + c16];
+                for (int J = 0; J < 2; J++) pa[J] = T[i * kTp + 16 * J + t_col(s, c16, q4)];
                 const float* dr = dhr + min(i, kTok - 1) * kEmb;
                 const float db[2] = {dr[c16], dr[min(16 + c16, kEmb - 1)]};
 #pragma unroll
@@ -1226,7 +1265,7 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
                 if (16 * I + c16 < 24)
 #pragma unroll
                     for (int J = 0; J < 2; J++)
-                        *reinterpret_cast<f32x4_t*>(T + (16 * I + c16) * kTp + 16 * J + 4 * q4) = dS[J][I];
+                        t_store(T + (16 * I + c16) * kTp + 16 * J + 4 * q4, dS[J][I], t_sw(c16));
             wave_sync();
             // ---- dK = dS^T Q: rows j, columns a (10 of 16); k = i = kh_row(s, q4) ----
             // ---- dQ^T = K^T dS^T: rows a = 4 q4 + g (10 of 16), columns i; k = j = kh_row(s, q4): B = dS^T rows
@@ -1237,10 +1276,15 @@ __global__ __launch_bounds__(kMThreads) __attribute__((amdgpu_waves_per_eu(3))) 
             for (int s = 0; s < kKH; s++) {
                 const int i = kh_row(s, q4);
 #pragma unroll
-                for (int J = 0; J < 2; J++) dK[J] = mfma4(T[i * kTp + 16 * J + c16], qb[s], dK[J]);
+                for (int J = 0; J < 2; J++) dK[J] = mfma4(T[i * kTp + 16 * J + t_col(s, c16, q4)], qb[s], dK[J]);
 #pragma unroll
-                for (int I = 0; I < 2; I++)  // (query rows i >= 24 hold other words: their dQ columns are not kept)
-                    dQ[I] = mfma4(ka[s], T[(16 * I + c16) * kTp + i], dQ[I]);
+                for (int I = 0; I < 2; I++) {  // (query rows i >= 24 hold other words: their dQ columns are not kept)
+                    // word (row, i ^ L(row)): rows 16 I + c16 (L is c16's); i = 4 q4 + s (s < 4: the row base is a
+                    // multiple of 4, so the XOR applies to the whole index) or 16 + 4 (s - 4) + q4
+                    const int rb = (16 * I + c16) * kTp;
+                    const float tv = s < 4 ? T[(rb + 4 * q4 + t_sw(c16)) ^ s] : T[rb + 16 + 4 * (s - 4) + (q4 ^ t_sw(c16))];
+                    dQ[I] = mfma4(ka[s], tv, dQ[I]);
+                }
             }
             front_prio(2);
             wave_sync();  // T is dead: the reduction operands G = [dq | dk | dv] and dctx
