@@ -241,7 +241,17 @@ class PPO:
         if self.graph_rollout and self.step_events is None and self.device.type == "cuda":
             return self._rollout_graph(b, n, T)
         with x3.cached_packs():  # the weights are fixed during the rollout: pack them once, not per step
+            return self._rollout_steps_deferred(b, n, T)
+
+    def _rollout_steps_deferred(self, b, n, T):
+        """_rollout_steps with the side-stream maze pre-generation queued once, after the last step
+        (VecMaze.defer_pregen): the steps' kernels get the GPU to themselves."""
+        self.venv.defer_pregen = True
+        try:
             return self._rollout_steps(b, n, T)
+        finally:
+            self.venv.defer_pregen = False
+            self.venv.flush_pregen()
 
     def _rollout_graph(self, b, n, T):
         """The rollout as a replay of a captured HIP graph (same kernels, same
@@ -253,7 +263,7 @@ class PPO:
             if not self._graph_warm:  # the first rollout runs uncaptured (one-time host work: kernel attributes)
                 self._graph_warm = True
                 with x3.cached_packs():
-                    return self._rollout_steps(b, n, T)
+                    return self._rollout_steps_deferred(b, n, T)
             self._graph = torch.cuda.CUDAGraph()
             self._ctr = torch.tensor([self._sample_offset], dtype=torch.int64, device=self.device)
             self._ctr_val = self._sample_offset

@@ -82,6 +82,12 @@ class VecMaze:
         # True while a HIP graph captures steps: the side-stream pre-generation is then kicked by the
         # caller after each replay instead (a captured fork must rejoin its origin stream)
         self.capturing = False
+        # True while a rollout runs its steps: the kicks only mark the side-stream generation pending and
+        # flush_pregen() queues one after the last step, so the generation (a ~1 ms latency-bound kernel)
+        # overlaps what follows the rollout instead of sharing the CUs with every step's kernels.  A maze
+        # that finishes twice inside one rollout generates its second maze in its reset (same maze).
+        self.defer_pregen = False
+        self._pregen_pending = False
         if self.pregen:
             self.next_layout = torch.ones((self.n, stride), dtype=torch.uint8, device=d)
             self.next_mazes = torch.zeros((self.n, 32), dtype=torch.uint8, device=d)
@@ -113,10 +119,19 @@ class VecMaze:
         generates it itself, or waits for the one in flight (gen_state)."""
         if not self.pregen or self.capturing:
             return
+        if self.defer_pregen:
+            self._pregen_pending = True
+            return
         cur = torch.cuda.current_stream(self.device)
         self._gen_stream.wait_stream(cur)
         with torch.cuda.stream(self._gen_stream):
             _lib.check(_lib.lib().mm_env_pregen(ctypes.byref(self._desc), _lib.stream_ptr()), "mm_env_pregen")
+
+    def flush_pregen(self):
+        """Queue the generation the deferred kicks left pending (defer_pregen)."""
+        if self._pregen_pending:
+            self._pregen_pending = False
+            self._kick_pregen()
 
     def _quiesce_pregen(self):
         """The current stream waits for the side stream (before the MT rows are rewritten)."""
