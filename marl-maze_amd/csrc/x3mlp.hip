@@ -1058,11 +1058,9 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     // EVERY OFFSET IS IN RANGE: lanes whose column is past N / K read the slice's first element (their
     // values only reach output rows >= N / columns >= K, which are never stored: an MFMA output element
     // depends on its own A row and B column only), and the rows past the slice in its last, partial step
-    // read it too and are zeroed by a select.  Out-of-range offsets (a load past num_records returns
-    // zeros) made this kernel return zeros in the last quarter-wave (lanes 48-63) of in-range loads of
-    // the same wave in ~3-60% of launches, depending on the form ("The k_wgrad_rect
-    // zeros"; tools/diag_wgrad_capture.py + tools/diag_wgrad_fit.py).  WG_OOB (diagnostic builds) restores
-    // the out-of-range offsets.
+    // read it too and are zeroed by a select.  (The round-4 forms, with out-of-range offsets or without,
+    // returned zeros in the last quarter-wave of some loads; the cause was operand registers rewritten
+    // while the loads were in flight: see the pinned operands below.)
     int loff[kPer], r8q[kPer], ldq[kPer];
     uint32_t voff[kPer];
     __amdgpu_buffer_rsrc_t rsq[kPer];
@@ -1073,11 +1071,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         const int e2 = isA ? e : e - itemsA, w = isA ? 16 * TN : 16 * NTK;
         const int c = e2 / w, j = e2 - c * w;
         const bool ok = e < items && (isA ? j < N : col0 + j < K);
-#ifdef WG_OOB
-        voff[q] = ok ? 4u * (uint32_t)(8 * c * (isA ? lddy : ldx) + j) : kBufOOB;
-#else
         voff[q] = ok ? 4u * (uint32_t)(8 * c * (isA ? lddy : ldx) + j) : 0u;
-#endif
         loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
         r8q[q] = 8 * c;
         // wave-uniform (itemsA = 64 TN), made scalar: a resource built from a divergent value becomes a
@@ -1096,26 +1090,41 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     // offset ob[q] is advanced IN PLACE one step at a time, just before the next batch (by then the
     // previous batch has landed: its values were converted and stored); the row strides i ld are scalar
     // offsets built once; ob, the strides and the resources are held live to the end of the kernel.
-    uint32_t ob[kPer], sri[kPer][8];
+    // x2 (235 VGPRs of accumulators and pieces): one VGPR offset per slot plus eight scalar row offsets
+    // i ld 4; x3 / f16 (VGPR room, and the scalar form spilled SGPRs in the f16 kernels -- a reloaded
+    // spill is a fresh temporary, rewritten right after the load): one VGPR offset per (slot, row i),
+    // each advanced in place.  tools/check_wgrad_operands.py checks the ISA of every instantiation.
+    constexpr bool kSOff = P == P_X2;
+    constexpr int kNv = kSOff ? 1 : 8;
+    uint32_t ob[kPer][kNv], sri[kPer][8];
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
-        ob[q] = voff[q];
 #pragma unroll
-        for (int i = 0; i < 8; i++) asm volatile("s_mul_i32 %0, %1, %2" : "=s"(sri[q][i]) : "s"(ldq[q]), "n"(4 * i));
+        for (int i = 0; i < kNv; i++) ob[q][i] = voff[q] + 4u * (uint32_t)(i * ldq[q]);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            if constexpr (kSOff) asm volatile("s_mul_i32 %0, %1, %2" : "=s"(sri[q][i]) : "s"(ldq[q]), "n"(4 * i));
+            else sri[q][i] = 0u;
+        }
     }
     auto hold_operands = [&]() {
 #pragma unroll
         for (int q = 0; q < kPer; q++) {
-            asm volatile("" ::"v"(ob[q]), "s"(rsq[q]));
+            asm volatile("" ::"s"(rsq[q]));
 #pragma unroll
-            for (int i = 0; i < 8; i++) asm volatile("" ::"s"(sri[q][i]));
+            for (int i = 0; i < kNv; i++) asm volatile("" ::"v"(ob[q][i]));
+            if constexpr (kSOff) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) asm volatile("" ::"s"(sri[q][i]));
+            }
         }
     };
     auto load_piece = [&](int q, int r0) {  // rows r0 + 8c .. + 7 of the slice; r0 = 0, 32, 64, .. in turn
         const int ld = ldq[q];
         if (r0 > 0) {
             __builtin_amdgcn_sched_barrier(0);
-            asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[q]) : "s"(128 * ld));
+#pragma unroll
+            for (int i = 0; i < kNv; i++) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[q][i]) : "s"(128 * ld));
         }
         if (r0 + 32 <= nrows) {  // a whole step inside the slice (wave-uniform)
 #pragma unroll
@@ -1123,7 +1132,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
 #ifdef WG_NO_GLOAD  // diagnostic builds only: no global loads
                 raw[q][i] = (float)(r0 + i);
 #else
-                raw[q][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsq[q], ob[q], sri[q][i], 0));
+                raw[q][i] = __uint_as_float(
+                    __builtin_amdgcn_raw_buffer_load_b32(rsq[q], ob[q][kSOff ? 0 : i], sri[q][i], 0));
 #endif
             }
         } else {  // the slice's last, partial step: rows past the slice read its first element, zeroed; these
@@ -1132,7 +1142,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 const float v = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(rsq[q], i < lim ? ob[q] + 4u * i * ld : 0u, 0, 0));
+                    __builtin_amdgcn_raw_buffer_load_b32(rsq[q], i < lim ? ob[q][0] + 4u * i * ld : 0u, 0, 0));
                 raw[q][i] = i < lim ? v : 0.f;
             }
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
@@ -1190,17 +1200,10 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     for (int q = 0; q < kPer; q++) load_piece(q, 0);
 #pragma unroll
     for (int q = 0; q < kPer; q++) store_piece_q(q, img);
-#ifndef WG_LATE_LOAD
     if (nsteps > 1) {
-#ifdef WG_LGKM0
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
-        __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
         for (int q = 0; q < kPer; q++) load_piece(q, 32);
     }
-#endif
     lds_barrier();
     // conversion of the next step's pieces: piece q at slot q * kEvery of the tile loop (VALU beside the
     // MFMAs), the rest after it
@@ -1213,6 +1216,17 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
 #else
     constexpr int kDone = 0;
 #endif
+    // Ping-pong (x2 / f16, whose conversion runs after the MFMAs): waves 4-7 -- each sharing its SIMD with one
+    // of waves 0-3 -- convert and stage the next step's pieces BEFORE their MFMAs, waves 0-3 after theirs, so
+    // on every SIMD one wave's MFMAs overlap the other's conversion VALU instead of both waves running the
+    // same phase at once.  The two halves touch different image sets (cur is read, nxt written), and each
+    // wave's loads still get one MFMA phase to arrive.  Measured slower (tools/ab_libs.py, 419,430 rows:
+    // x2 264 x 264 295 -> 311 us, 264 x 460 484 -> 532 us, f16 264 x 460 352 -> 368 us; x3 unchanged), so
+    // WG_PINGPONG=0 (every wave MFMAs first) is the default.
+#ifndef WG_PINGPONG
+#define WG_PINGPONG 0
+#endif
+    const bool conv_first = WG_PINGPONG && kDone == 0 && wave >= kWgWaves / 2;
     for (int st = 0; st < nsteps; st++) {
         const uint16_t* cur = img + (st & 1) * kSet;
         uint16_t* nxt = img + ((st + 1) & 1) * kSet;
@@ -1220,12 +1234,17 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         auto conv_at = [&](int slot) {
             if (kDone > 0 && more && slot % kEvery == 0 && slot / kEvery < kPer) store_piece_q(slot / kEvery, nxt);
         };
-#ifdef WG_LATE_LOAD  // diagnostic builds: the next step's loads issued after the barrier (none in flight across it)
-        if (more) {
+        auto stage_next = [&]() {  // the next step's pieces into nxt, then the loads of the step after it
+            if (more) {
 #pragma unroll
-            for (int q = 0; q < kPer; q++) load_piece(q, 32 * (st + 1));
-        }
-#endif
+                for (int q = kDone; q < kPer; q++) store_piece_q(q, nxt);
+                if (st + 2 < nsteps) {
+#pragma unroll
+                    for (int q = 0; q < kPer; q++) load_piece(q, 32 * (st + 2));
+                }
+            }
+        };
+        if (conv_first) stage_next();
 #ifndef WG_NO_MFMA
         if constexpr (RN > 0) {
             bf16x8 a[RN][3], b[2][3];
@@ -1253,24 +1272,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
             conv_at((RN > 0 ? NTK : 0) + e);
         }
 #endif
-        if (more) {
-#pragma unroll
-            for (int q = kDone; q < kPer; q++) store_piece_q(q, nxt);
-#ifndef WG_LATE_LOAD
-            if (st + 2 < nsteps) {
-#ifdef WG_LGKM0  // diagnostic builds: this wave's LDS writes completed before the loads issue
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0) only
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-#pragma unroll
-                for (int q = 0; q < kPer; q++) load_piece(q, 32 * (st + 2));
-            }
-#endif
-        }
-#ifdef WG_DRAIN  // diagnostic builds: every load landed before the barrier
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), lgkmcnt / expcnt untouched
-#endif
+        if (!conv_first) stage_next();
         lds_barrier();
     }
     hold_operands();

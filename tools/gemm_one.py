@@ -1,7 +1,8 @@
 """One actor-trunk GEMM shape launched repeatedly (for rocprofv3 --pmc passes).
 
 SHAPE=NxK (default 264x264), M rows (default 419,430), PREC=x3|x2|f16, FORM=fwd (bias + ReLU +
-bits out) | bwd (bits in + column sums) | plain; MARLMAZE_GEMM_BRES=0 selects k_x3nt.
+bits out) | bwd (bits in + column sums) | plain | wgrad (dW [N, K] = dY^T X, dY [M, N], X [M, K]);
+MARLMAZE_GEMM_BRES=0 selects k_x3nt.
 """
 import os
 import sys
@@ -29,8 +30,14 @@ def main():
     cs = x3.colsum_buf(M, N, "cuda")
     ascale = 1.0
 
+    if form == "wgrad":
+        dy = torch.randn(M, N, device="cuda", generator=g) / M
+        dsc = 1.0 if prec == "x3" else float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
+
     def one():
-        if form == "fwd":
+        if form == "wgrad":
+            x3.wgrad(dy, a, prec=prec, dscale=dsc)
+        elif form == "fwd":
             x3.gemm(a, w, bias=bias, relu=True, mbits_out=mb, out=out)
         elif form == "bwd":
             x3.gemm(a, w, mbits_in=mb, colsum=cs, ascale=ascale, out=out)
