@@ -308,14 +308,43 @@ int mm_gemm_wgrad_slices(int prec, int M, int N, int K);
 int mm_gemm_wgrad_partials(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N,
                            int K, float cscale, float* ws, void* stream);
 /* Range guard of MM_PREC_X2 / MM_PREC_F16 (fp16 planes: |x s| >= 65520 would
- * round to inf, where the fp32 reference stays finite).  Every kernel that
- * converts an operand to fp16 planes (mm_gemm_tp_pack(_multi), mm_gemm_nt,
- * mm_gemm_wgrad(_partials)) ORs bit 0 into a library-wide flag when a value it
- * converted had |x s| >= 2^15 (or was infinite); its result is then not to be
- * used -- redo the work at MM_PREC_X3 (fp32's range).
+ * round to inf, where the fp32 reference stays finite).  The GEMM and
+ * weight-gradient kernels of those precisions (mm_gemm_nt(_h),
+ * mm_gemm_wgrad(_h, _partials, _partials_h)) OR bit 0 into a library-wide flag
+ * when an output accumulator is not finite -- an operand that left fp16's
+ * range always makes one -- or, for fp16 outputs (MM_GEMM_C_F16), when a
+ * stored value overflowed fp16; the result is then not to be used: redo the
+ * work at MM_PREC_X3 (fp32's range).
  * mm_gemm_range_flag: stream-ordered; writes the flag to out[0] (device
  * memory, may be NULL) and, when clear != 0, resets it. */
 int mm_gemm_range_flag(uint32_t* out, int clear, void* stream);
+
+/* fp16 activation storage of the MM_PREC_F16 networks (BASELINE configs[4]):
+ * the next GEMM rounds every activation to fp16 anyway, so storing them at that
+ * precision gives the same operands at half the bytes.  Replaces nothing in
+ * the reference (its networks are fp32, networks.py:31-41); used by the
+ * update's f16 forward / backward only.
+ * mm_gemm_nt_h: mm_gemm_nt with flags -- MM_GEMM_A_F16: a is fp16 [M, lda]
+ *   (MM_PREC_F16, ascale 1, K and lda multiples of 4; the B-resident kernel:
+ *   mm_gemm_a16_ok says whether the shape takes it); MM_GEMM_C_F16: c is fp16
+ *   [M, ldc], the forward with mbits_out only.
+ * mm_gemm_wgrad_h / mm_gemm_wgrad_partials_h: with MM_GEMM_B_F16, x is fp16
+ *   [M, ldx] (MM_PREC_F16 at the update's shapes; MM_PREC_X3 for N <= 16,
+ *   K <= 272: the actor heads).
+ * mm_heads_fwd_h16: mm_heads_fwd over fp16 h (K 257..288). */
+#define MM_GEMM_A_F16 1
+#define MM_GEMM_C_F16 2
+#define MM_GEMM_B_F16 4
+int mm_gemm_nt_h(int prec, int flags, const void* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
+                 const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out, float* colsum,
+                 float cscale, void* c, int ldc, void* stream);
+int mm_gemm_a16_ok(int M, int N, int K, int lda, int ldc);
+int mm_gemm_wgrad_h(int prec, int flags, const float* dy, int lddy, float dscale, const void* x, int ldx, int M, int N,
+                    int K, float cscale, float* ws, float* dw, void* stream);
+int mm_gemm_wgrad_partials_h(int prec, int flags, const float* dy, int lddy, float dscale, const void* x, int ldx,
+                             int M, int N, int K, float cscale, float* ws, void* stream);
+int mm_heads_fwd_h16(const void* h, int ldh, int K, const float* w, const float* b, int M, float* logits,
+                     void* stream);
 
 /* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
  * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),

@@ -383,7 +383,8 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_head_sample(const float* 
 // streaming GEMV (443 MB of h per 419,430-row minibatch): NS (= ceil(K / 32)) 16-byte loads per lane all in
 // flight, through a buffer resource (columns past K and rows past M read zeros: no exec-masked loads), head
 // weights zero-padded in LDS.  NS = 0: a runtime loop for other widths.
-template <int NS>
+// H16: h is fp16 (the f16 networks' stored activations; exact in fp32, so the arithmetic is unchanged)
+template <int NS, bool H16 = false>
 __global__ __launch_bounds__(kHsLanes* kHsRows) void k_heads_fwd(const float* __restrict__ h, int ldh, int K,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ b, int M,
@@ -410,16 +411,27 @@ __global__ __launch_bounds__(kHsLanes* kHsRows) void k_heads_fwd(const float* __
     float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (NS > 0) {
         // gfx9 buffer resource word 3 0x00020000: 32-bit data format, raw addressing
+        constexpr uint32_t esz = H16 ? 2u : 4u;
         const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)h, (short)0, (int)((size_t)M * ldh * 4), 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void*)h, (short)0, (int)((size_t)M * ldh * esz), 0x00020000);
         float4 hv[NS];
 #pragma unroll
         for (int s = 0; s < NS; s++) {
             const int c = 4 * j + 32 * s;
-            const uint32_t off = (row < M && c < K) ? 4u * ((uint32_t)row * (uint32_t)ldh + (uint32_t)c) : 0x80000000u;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-            hv[s] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
-                                __uint_as_float(v[3]));
+            const uint32_t off = (row < M && c < K) ? esz * ((uint32_t)row * (uint32_t)ldh + (uint32_t)c) : 0x80000000u;
+            if constexpr (H16) {
+                typedef __attribute__((ext_vector_type(2))) unsigned int u2;
+                typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+                // (the whole vector cast at once: __builtin_bit_cast of a vector ELEMENT (v.y) compiled to the
+                // first element's bits with this clang -- tests/test_gpu_f16_act.py caught it)
+                const u2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+                const h4 hh = __builtin_bit_cast(h4, v);
+                hv[s] = make_float4((float)hh.x, (float)hh.y, (float)hh.z, (float)hh.w);
+            } else {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+                hv[s] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                    __uint_as_float(v[3]));
+            }
         }
 #pragma unroll
         for (int s = 0; s < NS; s++) {
@@ -742,6 +754,19 @@ extern "C" int mm_heads_fwd(const float* h, int ldh, int K, const float* w, cons
         hipLaunchKernelGGL(k_heads_fwd<9>, grid, block, 0, (hipStream_t)stream, h, ldh, K, w, b, M, logits);
     else
         hipLaunchKernelGGL(k_heads_fwd<0>, grid, block, 0, (hipStream_t)stream, h, ldh, K, w, b, M, logits);
+    return (int)hipGetLastError();
+}
+
+// the same over fp16 h [M, ldh] (K = 257..288: the actor's 264-wide layer only)
+extern "C" int mm_heads_fwd_h16(const void* h, int ldh, int K, const float* w, const float* b, int M, float* logits,
+                                void* stream) {
+    if (!h || !w || !b || !logits || M < 0 || (K & 3) || (K + 31) / 32 != 9 || ldh < K || (ldh & 3) ||
+        ((uintptr_t)h & 7) || (size_t)M * ldh * 2 >= 0x80000000ull)
+        return MM_E_ARG;
+    if (M == 0) return 0;
+    const dim3 grid((M + kHsRows - 1) / kHsRows), block(kHsLanes * kHsRows);
+    hipLaunchKernelGGL((k_heads_fwd<9, true>), grid, block, 0, (hipStream_t)stream, static_cast<const float*>(h), ldh,
+                       K, w, b, M, logits);
     return (int)hipGetLastError();
 }
 

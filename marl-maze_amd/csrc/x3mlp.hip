@@ -333,6 +333,7 @@ struct Epi {
     int ldc, ldm, relu, cnks;  // cnks = TP column blocks of the output (ceil(N / 32))
     float cscale;              // P_F16: out = acc * cscale before bias (the inverse of the A scale)
     int bufok;                 // fp32 c (and colsum) addressable through buffer resources (< 2^31 bytes)
+    int c16;                   // c holds fp16 [M, ldc] (EM_FWD16: P_F16's forward activations)
 };
 
 // B piece i (column tile i / planes, plane i % planes) of k-step ks -> LDS (one 1-KiB LDS-DMA)
@@ -498,7 +499,10 @@ __device__ __forceinline__ void k_step(f32x4 (&acc)[NT], f32x4 (&accx)[NT], cons
 // Accumulators acc[c]: lane l holds rows 4 (l >> 4) + g, column 16 c + (l & 15).
 // fp32 rows are stored straight from the accumulators (16 lanes = 64 contiguous
 // bytes of a row); no workgroup barrier.
-enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3 };
+//   EM_FWD16: EM_FWD with fp16 out (P_F16: the update's activations stored at the operand precision --
+//             the next GEMM rounds them to fp16 anyway -- half the bytes of every activation read / write)
+enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3, EM_FWD16 = 4 };
+constexpr bool em_fwd(int em) { return em == EM_FWD || em == EM_FWD16; }
 
 template <int NT, int EM, int P>
 __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int M, int N, int col0, const Epi& ep,
@@ -631,10 +635,11 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
     int rq = 4 * (lane >> 4);
     asm volatile("" : "+v"(rq));  // offsets formed here, not hoisted over the main loop and held
     const int row0 = 16 * rt + rq, cl = lane & 15;
+    constexpr uint32_t esz = EM == EM_FWD16 ? 2u : 4u;  // bytes per output element
     uint32_t voff[4];
 #pragma unroll
-    for (int g = 0; g < 4; g++) voff[g] = 4u * ((uint32_t)(row0 + g) * (uint32_t)ep.ldc + (uint32_t)cl);
-    const int soff = 64 * tg0;  // bytes: the block's first column tile
+    for (int g = 0; g < 4; g++) voff[g] = esz * ((uint32_t)(row0 + g) * (uint32_t)ep.ldc + (uint32_t)cl);
+    const int soff = 16 * (int)esz * tg0;  // bytes: the block's first column tile
     uint32_t lbits[NW];
 #pragma unroll
     for (int w = 0; w < NW; w++) lbits[w] = 0u;
@@ -673,14 +678,20 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
             } else {
                 x += bv;
                 if (ep.relu) x = fmaxf(x, 0.f);
-                if (EM == EM_FWD) lbits[bit >> 5] |= (x > 0.f ? 1u : 0u) << (bit & 31);
+                if (em_fwd(EM)) lbits[bit >> 5] |= (x > 0.f ? 1u : 0u) << (bit & 31);
             }
-            uint32_t o = voff[g] + 64u * c;
+            uint32_t o = voff[g] + 16u * esz * c;
             if (part && col >= N) o = kBufOOB;
 #ifdef BRES_NO_STORE  // diagnostic builds only
             if (x == 1234.5f)
 #endif
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), crs, o, soff, 0);
+            if constexpr (EM == EM_FWD16) {
+                const _Float16 h = (_Float16)x;  // round to nearest; past 65504 it is inf: the range guard sees it
+                range_val<P>(rb, (float)h);
+                __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), crs, o, soff, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), crs, o, soff, 0);
+            }
         }
         if (EM == EM_BWD && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
             cs += __shfl_xor(cs, 16);
@@ -689,7 +700,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(cs), srs, so, 0, 0);
         }
     }
-    if (EM == EM_FWD) {
+    if (em_fwd(EM)) {
         uint8_t* mb = reinterpret_cast<uint8_t*>(ep.mbits_out + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
 #pragma unroll
         for (int m = 0; m < (CT + 1) / 2; m++)
@@ -725,8 +736,8 @@ __global__ __launch_bounds__(SW<P>::kThreads) void k_x3nt(const AT* __restrict__
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // (unused when !ep.bufok: then the ranges below are not consulted)
-    const __amdgpu_buffer_rsrc_t crs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * (EM == EM_FWD16 ? 2 : 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)ep.colsum, (short)0, (int)((size_t)((M + 15) / 16) * N * 4), 0x00020000);
     // workgroup g takes units g, g + G, ...  XCD-aware unit order: units u and
@@ -776,6 +787,8 @@ __global__ __launch_bounds__(SW<P>::kThreads) void k_x3nt(const AT* __restrict__
         // ---- epilogue (after the last k-step's barrier both stage buffers are free) ----
         if constexpr (EM == EM_TP) {
             epilogue_tp<NT>(acc, reinterpret_cast<float*>(sB0) + wave * 16 * 36, rt, M, N, ep, lane);
+        } else if constexpr (EM == EM_FWD16) {  // (the host requires bufok)
+            bres_epilogue<P, NT, EM>(acc, rt, cb * NT, NT, M, N, ep, crs, srs, sbias, lane);
         } else {
             if (ep.bufok && !ep.mask)  // buffer stores, one code path (bres_epilogue; tiles cb NT .. : even when bits)
                 bres_epilogue<P, NT, EM>(acc, rt, cb * NT, NT, M, N, ep, crs, srs, sbias, lane);
@@ -1029,11 +1042,20 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad(const float* __restrict__ 
 // (TN - 8 RN rows of NTK tiles, dealt round-robin: A and B read per tile).
 // No runtime branch in the MFMA loop.  Staging, double-buffered images,
 // partials and the reduction are those of k_wgrad.
-template <int P, int TN, int NTK>
+// a staged value from its dword: fp32 (esz 4), or the fp16 half at bit offset sh (esz 2) -- selects, no branch
+__device__ __forceinline__ float wg_val16(uint32_t d, uint32_t sh, bool h16) {
+    const float h = (float)__builtin_bit_cast(_Float16, (unsigned short)(d >> sh));
+    return h16 ? h : __uint_as_float(d);
+}
+
+// XB: bytes per X element -- 4 (fp32) or 2 (fp16: P_F16's stored activations, and the heads' x3 weight
+// gradient over them; fp16 values are exact in fp32, so the staging is that of their fp32 values)
+template <int P, int TN, int NTK, int XB = 4>
 __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restrict__ dy, int lddy, float dscale,
                                                            const float* __restrict__ x, int ldx, int M, int N, int K,
                                                            int rows, int nslices, int ncb, float cscale,
                                                            float* __restrict__ ws) {
+    static_assert(XB == 4 || (XB == 2 && P != P_X2), "fp16 X: P_F16 / P_X3");
     constexpr int kB = Prec<P>::kBlk;
     constexpr int np = Prec<P>::kPlanes;
     constexpr int RN = TN / kWgWaves;                               // n-tiles per wave in the rectangle
@@ -1051,7 +1073,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     const int m_begin = s * rows, nrows = min(M, m_begin + rows) - m_begin;
     const int col0 = cb * NTK * 16;
     const float* const baseA = dy + (size_t)m_begin * lddy;
-    const float* const baseB = x + (size_t)m_begin * ldx + col0;
+    const void* const baseB = reinterpret_cast<const char*>(x) + ((size_t)m_begin * ldx + col0) * XB;
 
     // loads through one buffer resource per piece slot q over the slice's rows (loop-invariant, built once),
     // the step's row offset added to the lane's VGPR offset -- no per-element branch or 64-bit address.
@@ -1062,7 +1084,9 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     // returned zeros in the last quarter-wave of some loads; the cause was operand registers rewritten
     // while the loads were in flight: see the pinned operands below.)
     int loff[kPer], r8q[kPer], ldq[kPer];
-    uint32_t voff[kPer];
+    uint32_t voff[kPer], eszq[kPer];  // eszq: bytes per element of the slot's operand (wave-uniform)
+    uint32_t hsh[kPer];               // XB 2, B slots: the bit offset of the lane's half in its dword
+    bool h16q[kPer];
     __amdgpu_buffer_rsrc_t rsq[kPer];
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
@@ -1071,15 +1095,21 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         const int e2 = isA ? e : e - itemsA, w = isA ? 16 * TN : 16 * NTK;
         const int c = e2 / w, j = e2 - c * w;
         const bool ok = e < items && (isA ? j < N : col0 + j < K);
-        voff[q] = ok ? 4u * (uint32_t)(8 * c * (isA ? lddy : ldx) + j) : 0u;
+        // fp16 X (XB 2): every load is a dword (one instruction form for A and B slots, no branch between
+        // load forms -- two forms merged at a branch made the compiler wait on each batch); the lane takes
+        // the half (j & 1) of the dword holding its element (ldx even: rows stay dword-aligned)
+        voff[q] = ok ? (isA ? 4u * (uint32_t)(8 * c * lddy + j) : (uint32_t)XB * (uint32_t)(8 * c * ldx + j) & ~3u) : 0u;
+        hsh[q] = (!isA && XB == 2 && ok) ? 16u * (uint32_t)(j & 1) : 0u;
+        h16q[q] = !isA && XB == 2;  // per lane (from threadIdx, not readfirstlane): a select, not a branch
         loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
         r8q[q] = 8 * c;
         // wave-uniform (itemsA = 64 TN), made scalar: a resource built from a divergent value becomes a
         // readfirstlane waterfall loop per load
         const bool isAu = __builtin_amdgcn_readfirstlane(threadIdx.x + kWgThreads * q) < itemsA;
         ldq[q] = isAu ? lddy : ldx;
-        rsq[q] = __builtin_amdgcn_make_buffer_rsrc((void*)(isAu ? baseA : baseB), (short)0,
-                                                   (int)(nrows * ldq[q] * 4), 0x00020000);
+        eszq[q] = isAu ? 4u : (uint32_t)XB;
+        rsq[q] = __builtin_amdgcn_make_buffer_rsrc(isAu ? (void*)baseA : (void*)baseB, (short)0,
+                                                   (int)(nrows * ldq[q] * eszq[q]), 0x00020000);
     }
     float raw[kPer][8];
 #ifndef WG_OLDFORM
@@ -1100,7 +1130,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
 #pragma unroll
     for (int q = 0; q < kPer; q++) {
 #pragma unroll
-        for (int i = 0; i < kNv; i++) ob[q][i] = voff[q] + 4u * (uint32_t)(i * ldq[q]);
+        for (int i = 0; i < kNv; i++) ob[q][i] = voff[q] + eszq[q] * (uint32_t)(i * ldq[q]);
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             if constexpr (kSOff) asm volatile("s_mul_i32 %0, %1, %2" : "=s"(sri[q][i]) : "s"(ldq[q]), "n"(4 * i));
@@ -1124,7 +1154,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         if (r0 > 0) {
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < kNv; i++) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[q][i]) : "s"(128 * ld));
+            for (int i = 0; i < kNv; i++)
+                asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[q][i]) : "s"(32 * (int)eszq[q] * ld));
         }
         if (r0 + 32 <= nrows) {  // a whole step inside the slice (wave-uniform)
 #pragma unroll
@@ -1132,20 +1163,26 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
 #ifdef WG_NO_GLOAD  // diagnostic builds only: no global loads
                 raw[q][i] = (float)(r0 + i);
 #else
-                raw[q][i] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(rsq[q], ob[q][kSOff ? 0 : i], sri[q][i], 0));
+                {
+                    const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rsq[q], ob[q][kSOff ? 0 : i], sri[q][i], 0);
+                    raw[q][i] = __uint_as_float(d);  // (fp16 X: the dword's bits; converted where consumed)
+                }
 #endif
             }
         } else {  // the slice's last, partial step: rows past the slice read its first element, zeroed; these
-                  // loads' offsets are temporaries, so they are waited for here (once per slice at most)
+                  // loads' offsets are temporaries, so they are waited for here (once per slice at most; the
+                  // previous batch has landed -- it was converted and stored just before -- so nothing is in
+                  // flight while the temporaries live: the markers let tools/check_wgrad_operands.py skip them)
+            asm volatile(";;wg-partial-begin");
             const int lim = nrows - r0 - r8q[q];
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                const float v = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(rsq[q], i < lim ? ob[q][0] + 4u * i * ld : 0u, 0, 0));
-                raw[q][i] = i < lim ? v : 0.f;
+                const uint32_t o = i < lim ? ob[q][0] + eszq[q] * i * ld : 0u;
+                const uint32_t d = __builtin_amdgcn_raw_buffer_load_b32(rsq[q], o, 0, 0);
+                raw[q][i] = i < lim ? __uint_as_float(d) : 0.f;  // (fp16 X: bits, converted where consumed; 0 -> 0)
             }
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+            asm volatile(";;wg-partial-end");
         }
     };
 #else  // diagnostic builds: the round-4 form (offsets recomputed per batch, registers reused by the compiler)
@@ -1177,7 +1214,15 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     auto store_piece_q = [&](int q, uint16_t* dst_set) {
         if (threadIdx.x + kWgThreads * q < items) {
             const bool isA = threadIdx.x + kWgThreads * q < itemsA;
-            store_piece<P>(raw[q], isA ? dscale : 1.f, reinterpret_cast<uint4*>(dst_set + loff[q]));
+            if constexpr (XB == 2) {  // the fp16 halves of the loaded dwords, here where they are consumed (a
+                                      // conversion right after the load would wait for it there)
+                float v[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) v[i] = wg_val16(__float_as_uint(raw[q][i]), hsh[q], h16q[q]);
+                store_piece<P>(v, isA ? dscale : 1.f, reinterpret_cast<uint4*>(dst_set + loff[q]));
+            } else {
+                store_piece<P>(raw[q], isA ? dscale : 1.f, reinterpret_cast<uint4*>(dst_set + loff[q]));
+            }
         }
     };
     auto lds_barrier = [&]() {
@@ -1397,6 +1442,14 @@ __device__ __forceinline__ void bres_load(const BresA& as, int ks, int K, int kq
         const int kk = 32 * ks + kq + 16 * h;
 #pragma unroll
         for (int r = 0; r < RT; r++) {
+            if constexpr (VW == 16) {  // fp16 A: the 4 halves k .. k + 3 as 8 bytes; r[.][0] packs both halves'
+                const uint32_t o = as.roff[r] + 2u * (32 * ks + 16 * h);
+                const u32x2v v = __builtin_amdgcn_raw_buffer_load_b64(as.rsrc, kk < K ? o : kBufOOB, 0, 0);
+                if (h == 0) raw[r][0].x = __uint_as_float(v.x), raw[r][0].y = __uint_as_float(v.y);
+                else raw[r][0].z = __uint_as_float(v.x), raw[r][0].w = __uint_as_float(v.y);
+                raw[r][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                continue;
+            }
             const uint32_t o = as.roff[r] + 4u * (32 * ks + 16 * h);
             if constexpr (VW == 4) {
                 const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(as.rsrc, kk < K ? o : kBufOOB, 0, 0);
@@ -1413,8 +1466,13 @@ __device__ __forceinline__ void bres_load(const BresA& as, int ks, int K, int kq
 }
 
 // 8 fp32 -> the precision's A fragment planes (P_X3: exact three-way split; P_F16: x * s rounded)
-template <int P>
+template <int P, int VW>
 __device__ __forceinline__ void bres_frag(const float4 (&r)[2], float s, bf16x8 (&a)[3]) {
+    if constexpr (VW == 16) {  // fp16 A (P_F16, scale 1): the loaded halves are the fragment
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(r[0].x), __float_as_uint(r[0].y),
+                                                     __float_as_uint(r[0].z), __float_as_uint(r[0].w)));
+        return;
+    }
 #ifdef BRES_NO_SPLIT  // diagnostic builds only: the raw bits as fragments (no split VALU; outputs wrong)
     a[0] = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(r[0].x), __float_as_uint(r[0].y),
                                                  __float_as_uint(r[1].x), __float_as_uint(r[1].y)));
@@ -1447,8 +1505,12 @@ __device__ __forceinline__ void bres_frag(const float4 (&r)[2], float s, bf16x8 
 }
 
 // the final 16-wide step: the 4 values k = 4 (l >> 4) .. +3 (the j < 4 half of a TP piece)
-template <int P>
+template <int P, int VW>
 __device__ __forceinline__ void bres_frag16(const float4& r, float s, uint2 (&a)[3]) {
+    if constexpr (VW == 16) {  // fp16 A: the j < 4 half is the first 8 bytes
+        a[0] = make_uint2(__float_as_uint(r.x), __float_as_uint(r.y));
+        return;
+    }
     if constexpr (P == P_X3) {
         uint32_t h[2], m[2], l[2];
         split2(r.x, r.y, h[0], m[0], l[0]);
@@ -1509,7 +1571,7 @@ __device__ __forceinline__ void bres_step(f32x4 (&acc)[RT][CT], f32x4 (&accx)[RT
     constexpr int np = Prec<P>::kPlanes;
     bf16x8 a[RT][3];
 #pragma unroll
-    for (int r = 0; r < RT; r++) bres_frag<P>(cur[r], ascale, a[r]);
+    for (int r = 0; r < RT; r++) bres_frag<P, VW>(cur[r], ascale, a[r]);
     bres_load<RT, VW>(as, ks + D, K, kq, nxt);  // D steps ahead (past the last step: zeros)
     int boff = ((ks * ctb + c0) * np) * 64 + lane;  // bf16x8 units
     asm volatile("" : "+v"(boff));                  // one base per step (not 18 hoisted addresses)
@@ -1553,7 +1615,8 @@ template <int P, int CT, int RT, int EM, int VW>
 __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restrict__ A, int lda, float ascale,
                                                    const uint16_t* __restrict__ B, int M, int N, int K, int nks,
                                                    BresPlan pl, Epi ep) {
-    static_assert(EM == EM_F32 || EM == EM_FWD || EM == EM_BWD, "fp32 outputs");
+    static_assert(EM == EM_F32 || EM == EM_FWD || EM == EM_BWD || EM == EM_FWD16, "row-major outputs");
+    static_assert(VW != 16 || P == P_F16, "fp16 A: P_F16");
     constexpr int np = Prec<P>::kPlanes;
     extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
     const int lane = threadIdx.x & 63;
@@ -1603,10 +1666,12 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
     const int nsb = (ctb + CT - 1) / CT;
     const int kq = 4 * (lane >> 4);
     // gfx9 buffer resource word 3 0x00020000: 32-bit data format, raw (stride 0) addressing
+    constexpr uint32_t aesz = VW == 16 ? 2u : 4u;  // VW 16: A is fp16 [M, lda]
     const __amdgpu_buffer_rsrc_t arsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((size_t)M * lda * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((size_t)M * lda * aesz), 0x00020000);
     const __amdgpu_buffer_rsrc_t crs =  // C [M, ldc]: rows past M past num_records
-        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * 4), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * (EM == EM_FWD16 ? 2 : 4)),
+                                          0x00020000);
     const __amdgpu_buffer_rsrc_t srs =  // colsum [ceil(M / 16), N]
         __builtin_amdgcn_make_buffer_rsrc((void*)ep.colsum, (short)0, (int)((size_t)((M + 15) / 16) * N * 4),
                                           0x00020000);
@@ -1622,7 +1687,7 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
 #else
             const int row = min(16 * (RT * u + r) + (lane & 15), M - 1);  // rows past M: computed, not stored
 #endif
-            as.roff[r] = 4u * ((uint32_t)row * (uint32_t)lda + (uint32_t)kq);
+            as.roff[r] = aesz * ((uint32_t)row * (uint32_t)lda + (uint32_t)kq);
         }
         for (int s = 0; s < nsb; s++) {
             const int c0 = s * CT, ctn = min(CT, ctb - c0);
@@ -1652,7 +1717,7 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
                 if (half) {  // step nfull is in A (rem 0), B (rem 1) or C (rem 2)
 #pragma unroll
                     for (int r = 0; r < RT; r++)
-                        bres_frag16<P>(rem == 0 ? rA[r][0] : rem == 1 ? rB[r][0] : rC[r][0], ascale, a4[r]);
+                        bres_frag16<P, VW>(rem == 0 ? rA[r][0] : rem == 1 ? rB[r][0] : rC[r][0], ascale, a4[r]);
                 }
             } else {
                 float4 rawA[RT][2], rawB[RT][2];
@@ -1666,7 +1731,7 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
                 if (odd) bres_step<P, CT, RT, VW>(acc, accx, rawA, rawB, as, ks, K, kq, ctb, c0, ctn, ascale, sF, lane);
                 if (half) {
 #pragma unroll
-                    for (int r = 0; r < RT; r++) bres_frag16<P>(odd ? rawB[r][0] : rawA[r][0], ascale, a4[r]);
+                    for (int r = 0; r < RT; r++) bres_frag16<P, VW>(odd ? rawB[r][0] : rawA[r][0], ascale, a4[r]);
                 }
             }
             if (half) {
@@ -1798,6 +1863,15 @@ static int launch_nt(const AT* a, int lda, float ascale, const uint16_t* b, int 
             return (int)hipGetLastError();
         }
     } else if (ep.ctp) {
+        return MM_E_ARG;
+    }
+    if (ep.c16) {  // fp16 activations out: P_F16's forward with bits, through the buffer-store epilogue
+        if constexpr (P == P_F16) {
+            if (!ep.mbits_out || !ep.bufok) return MM_E_ARG;
+            hipLaunchKernelGGL((k_x3nt<NT, P, AS, AT, EM_FWD16>), dim3(grid), dim3(kT), 0, s, a, lda, ascale, b, M, N,
+                               K, nks, nrb, ncb, ep);
+            return (int)hipGetLastError();
+        }
         return MM_E_ARG;
     }
     if (ep.mbits_out)
@@ -1985,6 +2059,11 @@ static int launch_bres(const float* a, int lda, float ascale, const uint16_t* b,
 template <int P, int C, int VW>
 static int dispatch_bres_c(const float* a, int lda, float ascale, const uint16_t* b, int M, int N, int K,
                            const BresPlan& pl, const Epi& ep, hipStream_t s) {
+    if (ep.c16) {
+        if constexpr (P == P_F16)
+            if (ep.mbits_out) return launch_bres<P, C, EM_FWD16, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+        return MM_E_ARG;
+    }
     if (ep.mbits_out) return launch_bres<P, C, EM_FWD, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
     if (ep.mbits_in) return launch_bres<P, C, EM_BWD, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
     return launch_bres<P, C, EM_F32, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
@@ -2021,21 +2100,27 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
     if (!a_tp || ((uintptr_t)a_tp & 15)) return MM_E_ARG;
     if (M == 0) return 0;
     Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32, 1.f,
-           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31)};
+           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31), 0};
     return dispatch_nt<P_X3, ASrcTP>(a_tp, 0, 1.f, b_tp, M, N, K, ep, (hipStream_t)stream);
 }
 
 static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
                         const float* bias, int relu, const float* mask, int ldm, const uint32_t* mbits_in,
                         uint32_t* mbits_out, float* colsum, float cscale, float* c, int ldc, uint16_t* c_tp,
-                        void* stream) {
+                        void* stream, int flags = 0) {
     int e = check_common(b_tp, M, N, K, mask, ldm, c, ldc, c_tp);
     if (e) return e;
     if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
+    const bool a16 = flags & MM_GEMM_A_F16, c16 = flags & MM_GEMM_C_F16;
+    if (flags & ~(MM_GEMM_A_F16 | MM_GEMM_C_F16)) return MM_E_ARG;
+    // fp16 activations (P_F16 only): A fp16 at scale 1 on the B-resident kernel; C fp16 for the forward with bits
+    if ((a16 || c16) && (prec != MM_PREC_F16 || mask || c_tp)) return MM_E_ARG;
+    if (a16 && (ascale != 1.f || (K & 3) || (lda & 3) || ((uintptr_t)a & 7))) return MM_E_ARG;
+    if (c16 && (!mbits_out || ((uintptr_t)c & 1))) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (ascale != 1.f || cscale != 1.f)) return MM_E_ARG;  // the split is exact: no scaling
-    const bool v4 = !(K & 3) && !(lda & 3) && !((uintptr_t)a & 15);
-    const bool v2 = !(K & 1) && !(lda & 1) && !((uintptr_t)a & 7);
-    if (!a || lda < K || !(v4 || v2) || (!v4 && N > 64)) return MM_E_ARG;  // 8-byte rows: narrow outputs only
+    const bool v4 = !a16 && !(K & 3) && !(lda & 3) && !((uintptr_t)a & 15);
+    const bool v2 = !a16 && !(K & 1) && !(lda & 1) && !((uintptr_t)a & 7);
+    if (!a || lda < K || !(v4 || v2 || a16) || (!v4 && !a16 && N > 64)) return MM_E_ARG;  // 8-byte rows: narrow outputs only
     if ((mbits_in || mbits_out) && (N > 16 * 17 || c_tp || mask || (mbits_in && mbits_out))) return MM_E_ARG;
     if (mbits_in && (bias || relu)) return MM_E_ARG;  // the input-gradient form: no bias, no ReLU of its own
     if (colsum && (!mbits_in || !c)) return MM_E_ARG;
@@ -2049,19 +2134,26 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
         for (size_t m0 = 0; m0 < (size_t)M; m0 += cap) {
             const int mr = (int)std::min(cap, (size_t)M - m0);
             const size_t rt0 = m0 / 16;
-            const int rc = gemm_nt_f32a(prec, a + m0 * lda, lda, ascale, b_tp, mr, N, K, bias, relu,
+            const float* am = reinterpret_cast<const float*>(reinterpret_cast<const char*>(a) + m0 * lda * (a16 ? 2 : 4));
+            float* cm = reinterpret_cast<float*>(reinterpret_cast<char*>(c) + m0 * ldc * (c16 ? 2 : 4));
+            const int rc = gemm_nt_f32a(prec, am, lda, ascale, b_tp, mr, N, K, bias, relu,
                                         mask ? mask + m0 * ldm : nullptr, ldm,
                                         mbits_in ? mbits_in + rt0 * 64 * kMaskWords : nullptr,
                                         mbits_out ? mbits_out + rt0 * 64 * kMaskWords : nullptr,
-                                        colsum ? colsum + rt0 * N : nullptr, cscale, c + m0 * ldc, ldc, nullptr, stream);
+                                        colsum ? colsum + rt0 * N : nullptr, cscale, cm, ldc, nullptr, stream, flags);
             if (rc) return rc;
         }
         return 0;
     }
-    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale, c != nullptr};
+    Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale, c != nullptr,
+           c16 ? 1 : 0};
     hipStream_t s = (hipStream_t)stream;
     BresPlan pl;
     int cfg = C_NARROW;
+    if (a16) {  // fp16 A: the B-resident kernel only
+        if (!bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) return MM_E_ARG;
+        return dispatch_bres<P_F16, 16>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s);
+    }
     if (!mask && !c_tp && bres_enabled() && bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) {
         if (prec == MM_PREC_X3)
             return v4 ? dispatch_bres<P_X3, 4>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s)
@@ -2098,6 +2190,14 @@ extern "C" int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const
     if (!c) return MM_E_ARG;
     return gemm_nt_f32a(prec, a, lda, ascale, b_tp, M, N, K, bias, relu, nullptr, 0, mbits_in, mbits_out, colsum,
                         cscale, c, ldc, nullptr, stream);
+}
+
+extern "C" int mm_gemm_nt_h(int prec, int flags, const void* a, int lda, float ascale, const uint16_t* b_tp, int M,
+                            int N, int K, const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out,
+                            float* colsum, float cscale, void* c, int ldc, void* stream) {
+    if (!c) return MM_E_ARG;
+    return gemm_nt_f32a(prec, static_cast<const float*>(a), lda, ascale, b_tp, M, N, K, bias, relu, nullptr, 0,
+                        mbits_in, mbits_out, colsum, cscale, static_cast<float*>(c), ldc, nullptr, stream, flags);
 }
 
 // dY = (dz W) * bits (the heads' backward through the last ReLU, bits from the
@@ -2200,34 +2300,45 @@ static int launch_wgrad(const WgPlan& p, const float* dy, int lddy, float dscale
 }
 
 // the structured kernel for the (TN, NTK) blocks the actor and critic produce; 1 = no instantiation
-template <int P, int TN, int NTK>
+template <int P, int TN, int NTK, int XB = 4>
 static int launch_rect_t(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
                          int N, int K, float cscale, float* ws, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)k_wgrad_rect<P, TN, NTK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)k_wgrad_rect<P, TN, NTK, XB>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess)
             return MM_E_ARG;
         attr = true;
     }
     const size_t lds = (size_t)2 * (TN + NTK) * Prec<P>::kBlk * sizeof(uint16_t);
-    hipLaunchKernelGGL((k_wgrad_rect<P, TN, NTK>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s, dy,
+    hipLaunchKernelGGL((k_wgrad_rect<P, TN, NTK, XB>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s, dy,
                        lddy, dscale, x, ldx, M, N, K, p.rows, p.nslices, p.ncb, cscale, ws);
     return (int)hipGetLastError();
 }
 
-template <int P>
+template <int P, int XB = 4>
 static int launch_rect_p(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
                          int N, int K, float cscale, float* ws, hipStream_t s) {
-#define MM_WR(a, b) \
-    if (p.TN == a && p.NTK == b) return launch_rect_t<P, a, b>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
-    MM_WR(17, 9) MM_WR(17, 8) MM_WR(1, 17) MM_WR(4, 9) MM_WR(4, 4) MM_WR(1, 4)
+#define MM_WR(a, b)                                                                                              \
+    if (p.TN == a && p.NTK == b)                                                                                 \
+        return launch_rect_t<P, a, b, XB>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+    if constexpr (XB == 2 && P == P_X3) {  // fp16 X at x3: the actor heads' weight gradient over h3 only
+        MM_WR(1, 17)
+    } else {
+        MM_WR(17, 9) MM_WR(17, 8) MM_WR(1, 17) MM_WR(4, 9) MM_WR(4, 4) MM_WR(1, 4)
+    }
 #undef MM_WR
-    return 1;
+    return XB == 2 ? MM_E_ARG : 1;  // fp16 X: no generic-kernel fallback
 }
 
 static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int lddy, float dscale, const float* x,
-                             int ldx, int M, int N, int K, float cscale, float* ws, hipStream_t s) {
+                             int ldx, int M, int N, int K, float cscale, float* ws, hipStream_t s, bool x16 = false) {
+    if (x16) {  // fp16 X (P_F16 / P_X3): the structured kernel only
+        if ((size_t)M * lddy * 4 >= ((size_t)1 << 31) || (size_t)M * ldx * 2 >= ((size_t)1 << 31)) return MM_E_ARG;
+        return prec == MM_PREC_X3    ? launch_rect_p<P_X3, 2>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
+               : prec == MM_PREC_F16 ? launch_rect_p<P_F16, 2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s)
+                                     : MM_E_ARG;
+    }
 #ifdef WG_GENERIC  // diagnostic builds: the generic kernel for every shape
     return 1;
 #endif
@@ -2239,8 +2350,10 @@ static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int ldd
 }
 
 static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
-                      float cscale, float* ws, float* dw, void* stream) {
+                      float cscale, float* ws, float* dw, void* stream, int flags = 0) {
     if (M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
+    if (flags & ~MM_GEMM_B_F16) return MM_E_ARG;
+    const bool x16 = flags & MM_GEMM_B_F16;
     if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (dscale != 1.f || cscale != 1.f)) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
@@ -2248,8 +2361,8 @@ static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const f
     if (!dy || !x || !ws) return MM_E_ARG;
     const WgPlan p = wg_plan(prec, M, N, K);
     if (!p.TPW) return MM_E_ARG;
-    int e = launch_wgrad_rect(prec, p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
-    if (e == 1)
+    int e = launch_wgrad_rect(prec, p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s, x16);
+    if (e == 1 && !x16)
         e = prec == MM_PREC_X3   ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
             : prec == MM_PREC_X2 ? launch_wgrad<P_X2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s)
                                  : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
@@ -2264,6 +2377,26 @@ extern "C" int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, 
                              int K, float cscale, float* ws, float* dw, void* stream) {
     if (!dw) return MM_E_ARG;
     return gemm_wgrad(prec, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, dw, stream);
+}
+
+extern "C" int mm_gemm_wgrad_h(int prec, int flags, const float* dy, int lddy, float dscale, const void* x, int ldx,
+                               int M, int N, int K, float cscale, float* ws, float* dw, void* stream) {
+    if (!dw) return MM_E_ARG;
+    return gemm_wgrad(prec, dy, lddy, dscale, static_cast<const float*>(x), ldx, M, N, K, cscale, ws, dw, stream,
+                      flags);
+}
+
+extern "C" int mm_gemm_wgrad_partials_h(int prec, int flags, const float* dy, int lddy, float dscale, const void* x,
+                                        int ldx, int M, int N, int K, float cscale, float* ws, void* stream) {
+    if (M <= 0) return MM_E_ARG;
+    return gemm_wgrad(prec, dy, lddy, dscale, static_cast<const float*>(x), ldx, M, N, K, cscale, ws, nullptr, stream,
+                      flags);
+}
+
+extern "C" int mm_gemm_a16_ok(int M, int N, int K, int lda, int ldc) {
+    BresPlan pl;
+    int cfg = C_NARROW;
+    return bres_enabled() && bres_plan(MM_PREC_F16, M, N, K, lda, ldc, true, pl, cfg) ? 1 : 0;
 }
 
 extern "C" int mm_gemm_wgrad_slices(int prec, int M, int N, int K) {

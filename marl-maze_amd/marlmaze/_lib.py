@@ -44,13 +44,15 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
            "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
            "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi", "mm_critic_value",
-           "mm_gemm_range_flag")
-VERSION = 304  # mm_version() this binding is written for
+           "mm_gemm_range_flag", "mm_gemm_nt_h", "mm_gemm_a16_ok", "mm_gemm_wgrad_h", "mm_gemm_wgrad_partials_h",
+           "mm_heads_fwd_h16")
+VERSION = 305  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16, PREC_X2 = 0, 1, 2  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
 FRONT_FWD = {"row1": 0, "row2": 1}  # MM_FRONT_FWD_*
 GEMM_ALGO = {"auto": 0, "stream": 1}  # MM_GEMM_*
+GEMM_A_F16, GEMM_C_F16, GEMM_B_F16 = 1, 2, 4  # MM_GEMM_A_F16 / _C_F16 / _B_F16
 
 
 class EnvDesc(ctypes.Structure):
@@ -198,6 +200,16 @@ def lib():
         L.mm_gemm_wgrad_partials.restype = i32
         L.mm_gemm_range_flag.argtypes = [P, i32, P]
         L.mm_gemm_range_flag.restype = i32
+        # (library 305's fp16-activation entry points; bound when present, so that tools/ab_libs.py can time
+        # an older build beside this one -- the product's build has them, tests/test_cpu_host.py checks)
+        for name, args in (("mm_gemm_nt_h", [i32, i32, P, i32, f32, P, i32, i32, i32, P, i32, P, P, P, f32, P, i32, P]),
+                           ("mm_gemm_a16_ok", [i32, i32, i32, i32, i32]),
+                           ("mm_gemm_wgrad_h", [i32, i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P, P]),
+                           ("mm_gemm_wgrad_partials_h", [i32, i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P]),
+                           ("mm_heads_fwd_h16", [P, i32, i32, P, P, i32, P, P])):
+            if hasattr(L, name):
+                getattr(L, name).argtypes = args
+                getattr(L, name).restype = i32
         L.mm_colsum_multi_ws_len.argtypes = [ctypes.POINTER(ColsumSeg), i32]
         L.mm_colsum_multi_ws_len.restype = ctypes.c_long
         L.mm_colsum_multi.argtypes = [ctypes.POINTER(ColsumSeg), i32, P, P]

@@ -221,9 +221,26 @@ def _wgrad(dy, x, prec, out=None):
     return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=_grad_scale(dy.shape[0], prec), out=out)
 
 
-def _mlp_fwd(h0, ws, bs, prec, need_bits):
+# f16 networks: the update's hidden activations are stored in fp16 (mm_gemm_nt_h) -- every consumer rounds
+# them to fp16 anyway (the next GEMM's operand, the weight gradients' X) or reads them exactly (the heads'
+# fp32 FMAs over fp16 values), so the arithmetic is that of fp32 storage at half the bytes.
+# MARLMAZE_F16_ACT=0 keeps them fp32 (A/B runs).
+F16_ACT = os.environ.get("MARLMAZE_F16_ACT", "1") != "0"
+
+
+def _act16(prec, M, widths, next_ks):
+    """fp16 storage of the hidden layers' outputs: f16, and every GEMM reading one takes fp16 A at that
+    shape (next_ks: (N, K) of those GEMMs)."""
+    from . import x3
+
+    return (F16_ACT and prec == "f16" and all(n % 4 == 0 for n in widths)
+            and all(x3.a16_ok(M, n, k) for n, k in next_ks))
+
+
+def _mlp_fwd(h0, ws, bs, prec, need_bits, act16=False):
     """The ReLU layers on the engine; returns the activations [h0, h1, ...] and
-    the forward GEMMs' ReLU bit masks (None without need_bits)."""
+    the forward GEMMs' ReLU bit masks (None without need_bits).  act16: the
+    layers' outputs in fp16 (f16 with bits only, see F16_ACT)."""
     from . import x3
 
     M, dev = h0.shape[0], h0.device
@@ -231,7 +248,8 @@ def _mlp_fwd(h0, ws, bs, prec, need_bits):
     h = h0
     for w, b in zip(ws, bs):
         mb = x3.mbits(M, dev) if need_bits else None
-        h = x3.gemm(h, x3.pack(w, prec=prec), bias=b, relu=True, mbits_out=mb)
+        out = torch.empty((M, w.shape[0]), dtype=torch.float16, device=dev) if act16 else None
+        h = x3.gemm(h, x3.pack(w, prec=prec), bias=b, relu=True, mbits_out=mb, out=out)
         hs.append(h)
         bits.append(mb)
     return hs, bits
@@ -266,6 +284,13 @@ def _heads_fwd(h, wh, bh):
     from . import _lib, x3
 
     M, K = h.shape
+    if h.dtype == torch.float16:  # the f16 networks' stored activations (fp32 FMAs over their exact values)
+        assert wh.shape[0] == 6 and (K + 31) // 32 == 9 and K % 4 == 0, (wh.shape, K)
+        h, wh, bh = h.contiguous(), wh.contiguous(), bh.contiguous()
+        out = torch.empty((M, 6), dtype=torch.float32, device=h.device)
+        _lib.check(_lib.lib().mm_heads_fwd_h16(_lib.ptr(h), K, K, _lib.ptr(wh), _lib.ptr(bh), M, _lib.ptr(out),
+                                                _lib.stream_ptr()), "mm_heads_fwd_h16")
+        return out
     if wh.shape[0] != 6 or K % 4 or K > 1024:
         return x3.gemm(h, x3.pack(wh, prec="x3"), bias=bh)
     h, wh, bh = h.contiguous(), wh.contiguous(), bh.contiguous()
@@ -336,11 +361,14 @@ class _EngineActor(torch.autograd.Function):
 
 def _critic_fwd(x, params, prec, need_bits, out=None):
     """networks.py:96-102 on the engine: x [M, 130] (8-byte rows) -> ReLU(64) ->
-    ReLU(64) -> V [M, 1] (into ``out`` [M, 1] when given)."""
+    ReLU(64) -> V [M, 1] (into ``out`` [M, 1] when given).  f16 with bits: the
+    hidden activations in fp16 (F16_ACT)."""
     from . import x3
 
     w0, b0, w1, b1, w2, b2 = params
-    hs, bits = _mlp_fwd(x, (w0, w1), (b0, b1), prec, need_bits)
+    act16 = need_bits and _act16(prec, x.shape[0], [w0.shape[0], w1.shape[0]],
+                                 [(w1.shape[0], w1.shape[1]), (w2.shape[0], w2.shape[1])])
+    hs, bits = _mlp_fwd(x, (w0, w1), (b0, b1), prec, need_bits, act16=act16)
     return x3.gemm(hs[-1], x3.pack(w2, prec=prec), bias=b2, out=out), hs, bits
 
 
@@ -512,7 +540,10 @@ class Actor(nn.Module):
         if not self._engine(h0):
             raise ValueError("Actor.train_forward needs the GPU engine's shapes (ReLU, widths <= 272)")
         params = self._mlp_params()
-        hs, bits = _mlp_fwd(h0, params[0::2], params[1::2], self.gemm_prec, True)
+        wl = [lin.weight for lin in self.layers]
+        act16 = (_act16(self.gemm_prec, h0.shape[0], [w_.shape[0] for w_ in wl],
+                        [(w_.shape[0], w_.shape[1]) for w_ in wl[1:]]) and (wl[-1].shape[0] + 31) // 32 == 9)
+        hs, bits = _mlp_fwd(h0, params[0::2], params[1::2], self.gemm_prec, True, act16=act16)
         w, b = self.heads()
         z = _heads_fwd(hs[-1], w, b)
         return z, (x, ws, hs, bits)

@@ -204,15 +204,30 @@ def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None
             res = gemm(a, pack(src, trans=trans, prec="x3"), bias, relu, mbits_in, mbits_out, colsum, 1.0, out)
         return res
     N, K = b.R, b.C
-    assert a.dtype == torch.float32 and a.dim() == 2 and a.stride(1) == 1 and a.shape[1] == K, (a.shape, K)
+    assert a.dtype in (torch.float32, torch.float16) and a.dim() == 2 and a.stride(1) == 1 and a.shape[1] == K, \
+        (a.dtype, a.shape, K)
     M = a.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    if a.dtype == torch.float16 or out.dtype == torch.float16:  # fp16 activations (f16 only: mm_gemm_nt_h)
+        assert b.prec == "f16" and out.dtype in (torch.float32, torch.float16), (b.prec, out.dtype)
+        flags = ((_lib.GEMM_A_F16 if a.dtype == torch.float16 else 0)
+                 | (_lib.GEMM_C_F16 if out.dtype == torch.float16 else 0))
+        _lib.check(_lib.lib().mm_gemm_nt_h(PRECS[b.prec], flags, _lib.ptr(a), a.stride(0), float(ascale), b.ptr(),
+                                           M, N, K, _lib.ptr(bias), int(relu), _lib.ptr(mbits_in),
+                                           _lib.ptr(mbits_out), _lib.ptr(colsum), 1.0 / float(ascale), _lib.ptr(out),
+                                           out.stride(0), _lib.stream_ptr()), "mm_gemm_nt_h")
+        return out
     _lib.check(_lib.lib().mm_gemm_nt(PRECS[b.prec], _lib.ptr(a), a.stride(0), float(ascale), b.ptr(), M, N, K,
                                      _lib.ptr(bias), int(relu), _lib.ptr(mbits_in), _lib.ptr(mbits_out),
                                      _lib.ptr(colsum), 1.0 / float(ascale), _lib.ptr(out), out.stride(0),
                                      _lib.stream_ptr()), "mm_gemm_nt")
     return out
+
+
+def a16_ok(M, N, K):
+    """Whether an f16 GEMM of that shape takes fp16 A (mm_gemm_a16_ok: the B-resident kernel's shapes)."""
+    return bool(_lib.lib().mm_gemm_a16_ok(int(M), int(N), int(K), int(K), int(N)))
 
 
 def range_flag(out=None, clear=True):
@@ -248,6 +263,8 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dy.stride(1) == 1 and x.stride(1) == 1
+    assert x.dtype in (torch.float32, torch.float16) and dy.dtype == torch.float32, (x.dtype, dy.dtype)
+    flags = _lib.GEMM_B_F16 if x.dtype == torch.float16 else 0  # fp16 X: f16 activations (x3 / f16 only)
     defer = bool(_DEFER) and out is not None and M > 0  # a result the caller reads now is never deferred
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
@@ -257,16 +274,18 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
         S = L.mm_gemm_wgrad_slices(PRECS[prec], M, N, K)
         _lib.check(S if S < 0 else 0, "mm_gemm_wgrad_slices")
         ws = torch.empty(S * N * K, dtype=torch.float32, device=dy.device)
-        _lib.check(L.mm_gemm_wgrad_partials(PRECS[prec], _lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x),
-                                            x.stride(0), M, N, K, 1.0 / float(dscale), _lib.ptr(ws),
-                                            _lib.stream_ptr()), "mm_gemm_wgrad_partials")
+        args = (_lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M, N, K, 1.0 / float(dscale),
+                _lib.ptr(ws), _lib.stream_ptr())
+        _lib.check(L.mm_gemm_wgrad_partials_h(PRECS[prec], flags, *args) if flags
+                   else L.mm_gemm_wgrad_partials(PRECS[prec], *args), "mm_gemm_wgrad_partials")
         d = _DEFER[-1]
         d.sums.append(_lib.WsumSeg(_lib.ptr(ws), N * K, S, _lib.ptr(out)))
         d.keep += [ws, out]
         return out
     ws = torch.empty(max(1, L.mm_gemm_wgrad_ws_len(M, N, K)), dtype=torch.float32, device=dy.device)
-    _lib.check(L.mm_gemm_wgrad(PRECS[prec], _lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M,
-                               N, K, 1.0 / float(dscale), _lib.ptr(ws), _lib.ptr(out), _lib.stream_ptr()),
+    args = (_lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M, N, K, 1.0 / float(dscale),
+            _lib.ptr(ws), _lib.ptr(out), _lib.stream_ptr())
+    _lib.check(L.mm_gemm_wgrad_h(PRECS[prec], flags, *args) if flags else L.mm_gemm_wgrad(PRECS[prec], *args),
                "mm_gemm_wgrad")
     return out
 

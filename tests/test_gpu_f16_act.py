@@ -1,0 +1,85 @@
+"""fp16 activation storage of the f16 networks (mm_gemm_nt_h, mm_gemm_wgrad_h, mm_heads_fwd_h16): every
+consumer rounds an activation to fp16 anyway or reads it exactly, so each fp16-storage form must equal the
+fp32-storage form on the same (fp16-representable) values BIT FOR BIT -- and the f16 update built on them
+stays at test_gpu_f16.py's bars against the fp32 oracle (that file runs with fp16 storage on)."""
+import pytest
+import torch
+
+from marlmaze import networks, x3
+
+pytestmark = pytest.mark.gpu
+
+M = 40000  # >= the B-resident kernel's row threshold (fp16 A runs there only)
+
+
+def _h16(M, K, g):
+    return torch.relu(torch.randn(M, K, device="cuda", generator=g)).half()
+
+
+@pytest.mark.parametrize("N,K", [(264, 264), (64, 64), (1, 64)])
+def test_gemm_fp16_a_equals_fp32_a(N, K):
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    a16 = _h16(M, K, g)
+    w = x3.pack(torch.randn(N, K, device="cuda", generator=g) * 0.1, prec="f16")
+    b = torch.randn(N, device="cuda", generator=g)
+    assert x3.a16_ok(M, N, K)
+    relu = N > 1
+    # (zeroed: the kernels leave the mask words' padding bits unwritten)
+    mb16, mb32 = (x3.mbits(M, "cuda").zero_(), x3.mbits(M, "cuda").zero_()) if relu else (None, None)
+    y16 = x3.gemm(a16, w, bias=b, relu=relu, mbits_out=mb16)
+    y32 = x3.gemm(a16.float(), w, bias=b, relu=relu, mbits_out=mb32)
+    assert torch.equal(y16, y32)
+    if relu:
+        assert torch.equal(mb16, mb32)
+
+
+@pytest.mark.parametrize("N,K", [(264, 460), (264, 264), (64, 130), (64, 64)])
+def test_gemm_fp16_out_is_rounded_fp32_out(N, K):
+    g = torch.Generator(device="cuda").manual_seed(7 * N + K)
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = x3.pack(torch.randn(N, K, device="cuda", generator=g) * 0.1, prec="f16")
+    b = torch.randn(N, device="cuda", generator=g)
+    mb16, mb32 = x3.mbits(M, "cuda").zero_(), x3.mbits(M, "cuda").zero_()  # (padding bits unwritten)
+    out16 = torch.empty(M, N, dtype=torch.float16, device="cuda")
+    y16 = x3.gemm(a, w, bias=b, relu=True, mbits_out=mb16, out=out16)
+    y32 = x3.gemm(a, w, bias=b, relu=True, mbits_out=mb32)
+    assert y16.dtype == torch.float16
+    assert torch.equal(y16, y32.half())
+    assert torch.equal(mb16, mb32)  # the bits come from the fp32 value (> 0), as without fp16 storage
+
+
+@pytest.mark.parametrize("prec,N,K", [("f16", 264, 264), ("f16", 64, 64), ("f16", 1, 64), ("x3", 6, 264)])
+def test_wgrad_fp16_x_equals_fp32_x(prec, N, K):
+    g = torch.Generator(device="cuda").manual_seed(3 * N + K)
+    dy = torch.randn(M, N, device="cuda", generator=g) / M
+    x16 = _h16(M, K, g)
+    s = networks._grad_scale(M, prec)
+    d16 = x3.wgrad(dy, x16, prec=prec, dscale=s)
+    d32 = x3.wgrad(dy, x16.float(), prec=prec, dscale=s)
+    assert torch.equal(d16, d32)
+
+
+def test_heads_fwd_fp16_h_equals_fp32_h():
+    g = torch.Generator(device="cuda").manual_seed(11)
+    h16 = _h16(M, 264, g)
+    w = torch.randn(6, 264, device="cuda", generator=g) * 0.1
+    b = torch.randn(6, device="cuda", generator=g)
+    assert torch.equal(networks._heads_fwd(h16, w, b), networks._heads_fwd(h16.float(), w, b))
+
+
+def test_f16_train_forward_stores_fp16_and_matches_fp32_storage(monkeypatch):
+    """The actor's f16 train_forward keeps fp16 hidden activations, each equal to the fp32-storage run's
+    rounded to fp16 (the next layer's f16 GEMM rounds its input the same way either way); the logits differ
+    only through the heads' fp32 FMAs reading the rounded last layer."""
+    torch.manual_seed(5)
+    actor = networks.Actor(hidden_sizes=(264, 264, 264), gemm_prec="f16").cuda()
+    x = torch.randn(M, 65, device="cuda")
+    z, saved = actor.train_forward(x)
+    hs = saved[2]
+    assert hs[0].dtype == torch.float32 and all(h.dtype == torch.float16 for h in hs[1:])
+    monkeypatch.setattr(networks, "F16_ACT", False)
+    z32, saved32 = actor.train_forward(x)
+    assert all(h.dtype == torch.float32 for h in saved32[2])
+    for h, h32 in zip(hs[1:], saved32[2][1:]):
+        assert torch.equal(h, h32.half())
+    assert torch.equal(z, z32) or (z - z32).abs().max() <= 2e-3 * z32.abs().max()

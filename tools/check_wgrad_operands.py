@@ -58,8 +58,12 @@ def main():
         body = asm[s0:end]
         # the staging loads: their VGPR offset is one the kernel advances in place (v_add_u32 vX, vX, s..)
         pinned = {m.group(1) for m in (re.match(r"\s+v_add_u32 (v\d+), \1, s\d+$", l) for l in body) if m}
-        first_use = {}  # operand register -> index of the first staging load reading it
+        first_use = {}  # operand register -> index of the first staging load reading it (outside the markers)
+        inpart = False
         for i, l in enumerate(body):
+            inpart = (inpart or ";;wg-partial-begin" in l) and ";;wg-partial-end" not in l
+            if inpart:
+                continue
             m = re.match(r"\s+buffer_load_dword (v\d+), (v\d+), (s\[\d+:\d+\]), (s\d+|0) offen", l)
             if m and m.group(2) in pinned:
                 for r in regs(m.group(2)) | regs(m.group(3)) | regs(m.group(4)):
@@ -68,7 +72,14 @@ def main():
         # it); hold_operands() keeps the operands live at least that far
         hold = max(i for i, l in enumerate(body) if "s_barrier" in l)
         hits = []
-        for i in range(len(body)):
+        skip = False  # inside the partial-step loads (the kernel's ;;wg-partial-begin / -end markers): nothing
+        for i in range(len(body)):  # is in flight there, and their temporaries are waited for (vmcnt(0))
+            if ";;wg-partial-begin" in body[i]:
+                skip = True
+            elif ";;wg-partial-end" in body[i]:
+                skip = False
+            if skip:
+                continue
             op, w = dst(body[i])
             for r in w:
                 if r in first_use and first_use[r] < i < hold and not (op == "v_add_u32" and len(w) == 1):
