@@ -324,20 +324,27 @@ int mm_gemm_range_flag(uint32_t* out, int clear, void* stream);
  * precision gives the same operands at half the bytes.  Replaces nothing in
  * the reference (its networks are fp32, networks.py:31-41); used by the
  * update's f16 forward / backward only.
+ * The input gradients likewise: stored fp16 as fp16(dY s) -- s the power-of-two
+ * scale their consumers apply anyway -- and read back with ascale / dscale 1.
  * mm_gemm_nt_h: mm_gemm_nt with flags -- MM_GEMM_A_F16: a is fp16 [M, lda]
  *   (MM_PREC_F16, ascale 1, K and lda multiples of 4; the B-resident kernel:
  *   mm_gemm_a16_ok says whether the shape takes it); MM_GEMM_C_F16: c is fp16
- *   [M, ldc], the forward with mbits_out only.
+ *   [M, ldc]: the forward with mbits_out, or the input gradient with mbits_in,
+ *   stored as fp16(out * oscale) (its column sums stay those of the fp32 out).
  * mm_gemm_wgrad_h / mm_gemm_wgrad_partials_h: with MM_GEMM_B_F16, x is fp16
  *   [M, ldx] (MM_PREC_F16 at the update's shapes; MM_PREC_X3 for N <= 16,
- *   K <= 272: the actor heads).
+ *   K <= 272: the actor heads); with MM_GEMM_A_F16, dy is fp16 [M, lddy]
+ *   (MM_PREC_F16; dscale 1 for a pre-scaled dY, cscale its inverse scale).
+ * mm_x3_heads_bwd_h16: mm_x3_heads_bwd writing dy fp16 = fp16(dY * oscale).
  * mm_heads_fwd_h16: mm_heads_fwd over fp16 h (K 257..288). */
 #define MM_GEMM_A_F16 1
 #define MM_GEMM_C_F16 2
 #define MM_GEMM_B_F16 4
 int mm_gemm_nt_h(int prec, int flags, const void* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
                  const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out, float* colsum,
-                 float cscale, void* c, int ldc, void* stream);
+                 float cscale, float oscale, void* c, int ldc, void* stream);
+int mm_x3_heads_bwd_h16(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N, void* dy,
+                        float* colsum, float oscale, void* stream);
 int mm_gemm_a16_ok(int M, int N, int K, int lda, int ldc);
 int mm_gemm_wgrad_h(int prec, int flags, const float* dy, int lddy, float dscale, const void* x, int ldx, int M, int N,
                     int K, float cscale, float* ws, float* dw, void* stream);

@@ -333,7 +333,8 @@ struct Epi {
     int ldc, ldm, relu, cnks;  // cnks = TP column blocks of the output (ceil(N / 32))
     float cscale;              // P_F16: out = acc * cscale before bias (the inverse of the A scale)
     int bufok;                 // fp32 c (and colsum) addressable through buffer resources (< 2^31 bytes)
-    int c16;                   // c holds fp16 [M, ldc] (EM_FWD16: P_F16's forward activations)
+    int c16;                   // c holds fp16 [M, ldc] (EM_FWD16 / EM_BWD16: P_F16's stored activations / gradients)
+    float oscale;              // EM_BWD16: c = fp16(out * oscale) (the input gradient pre-scaled for its consumers)
 };
 
 // B piece i (column tile i / planes, plane i % planes) of k-step ks -> LDS (one 1-KiB LDS-DMA)
@@ -501,8 +502,12 @@ __device__ __forceinline__ void k_step(f32x4 (&acc)[NT], f32x4 (&accx)[NT], cons
 // bytes of a row); no workgroup barrier.
 //   EM_FWD16: EM_FWD with fp16 out (P_F16: the update's activations stored at the operand precision --
 //             the next GEMM rounds them to fp16 anyway -- half the bytes of every activation read / write)
-enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3, EM_FWD16 = 4 };
+//   EM_BWD16: EM_BWD with fp16 out * oscale (P_F16: the input gradient stored pre-scaled, as its consumers'
+//             operands; the column sums stay those of the fp32 values)
+enum { EM_F32 = 0, EM_FWD = 1, EM_BWD = 2, EM_TP = 3, EM_FWD16 = 4, EM_BWD16 = 5 };
 constexpr bool em_fwd(int em) { return em == EM_FWD || em == EM_FWD16; }
+constexpr bool em_bwd(int em) { return em == EM_BWD || em == EM_BWD16; }
+constexpr bool em_16(int em) { return em == EM_FWD16 || em == EM_BWD16; }
 
 template <int NT, int EM, int P>
 __device__ __forceinline__ void epilogue_f32(const f32x4 (&acc)[NT], int rt, int M, int N, int col0, const Epi& ep,
@@ -635,7 +640,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
     int rq = 4 * (lane >> 4);
     asm volatile("" : "+v"(rq));  // offsets formed here, not hoisted over the main loop and held
     const int row0 = 16 * rt + rq, cl = lane & 15;
-    constexpr uint32_t esz = EM == EM_FWD16 ? 2u : 4u;  // bytes per output element
+    constexpr uint32_t esz = em_16(EM) ? 2u : 4u;  // bytes per output element
     uint32_t voff[4];
 #pragma unroll
     for (int g = 0; g < 4; g++) voff[g] = esz * ((uint32_t)(row0 + g) * (uint32_t)ep.ldc + (uint32_t)cl);
@@ -643,7 +648,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
     uint32_t lbits[NW];
 #pragma unroll
     for (int w = 0; w < NW; w++) lbits[w] = 0u;
-    if (EM == EM_BWD) {
+    if (em_bwd(EM)) {
         const uint8_t* mi =
             reinterpret_cast<const uint8_t*>(ep.mbits_in + ((size_t)rt * 64 + lane) * kMaskWords) + tg0 / 2;
 #pragma unroll
@@ -663,7 +668,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
         if (c >= ctn || 16 * (tg0 + c) >= N) continue;  // wave-uniform (continue: the loop stays unrolled)
         const int col = 16 * (tg0 + c) + cl;
         const bool part = 16 * (tg0 + c) + 16 > N;  // wave-uniform: a tile crossing N
-        const float bv = (EM != EM_BWD && ep.bias) ? sbl[16 * c] : 0.f;
+        const float bv = (!em_bwd(EM) && ep.bias) ? sbl[16 * c] : 0.f;
         float cs = 0.f;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -671,7 +676,7 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
             float x = acc[c][g];
             range_val<P>(rb, x);
             if (Prec<P>::kScaled) x *= ep.cscale;
-            if (EM == EM_BWD) {
+            if (em_bwd(EM)) {
                 const bool on = (lbits[bit >> 5] >> (bit & 31)) & 1u;
                 if (!on) x = 0.f;
                 cs += x;
@@ -685,15 +690,16 @@ __device__ __forceinline__ void bres_epilogue(const f32x4 (&acc)[CT], int rt, in
 #ifdef BRES_NO_STORE  // diagnostic builds only
             if (x == 1234.5f)
 #endif
-            if constexpr (EM == EM_FWD16) {
-                const _Float16 h = (_Float16)x;  // round to nearest; past 65504 it is inf: the range guard sees it
+            if constexpr (em_16(EM)) {
+                // round to nearest; past 65504 it is inf: the range guard sees it
+                const _Float16 h = (_Float16)(EM == EM_BWD16 ? x * ep.oscale : x);
                 range_val<P>(rb, (float)h);
                 __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, h), crs, o, soff, 0);
             } else {
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), crs, o, soff, 0);
             }
         }
-        if (EM == EM_BWD && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
+        if (em_bwd(EM) && ep.colsum) {  // the bias gradient's partial: this tile's 16-row column sums
             cs += __shfl_xor(cs, 16);
             cs += __shfl_xor(cs, 32);
             const uint32_t so = (lane < 16 && col < N) ? 4u * ((uint32_t)rt * (uint32_t)N + (uint32_t)col) : kBufOOB;
@@ -811,11 +817,13 @@ __global__ __launch_bounds__(SW<P>::kThreads) void k_x3nt(const AT* __restrict__
 // tile map as the GEMM epilogue (one wave per 16-row tile, lane l: rows
 // 4 (l >> 4) + g, columns 16 c + (l & 15)), so the mask bits line up; also the
 // per-tile column sums (the last layer's bias gradient, before the final sum).
+// D16: dY stored fp16 as fp16(dY * oscale) (P_F16's pre-scaled input gradients; the sums stay fp32)
 constexpr int kHeadsMaxJ = 8;
-template <int NT>
+template <int NT, bool D16 = false>
 __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz, int J, const float* __restrict__ W,
                                                    const uint32_t* __restrict__ bits, int M, int N,
-                                                   float* __restrict__ dy, float* __restrict__ colsum) {
+                                                   float* __restrict__ dy, float* __restrict__ colsum,
+                                                   float oscale = 1.f) {
     __shared__ float sw[kHeadsMaxJ][16 * NT];
     {  // loads batched ahead of the LDS writes (one L2 round trip per workgroup); 256 threads
         constexpr int kN = kHeadsMaxJ * 16 * NT, kPer = (kN + 255) / 256;
@@ -836,6 +844,7 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz,
     const int rt = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (16 * rt >= M) return;
     const int rq = 4 * (lane >> 4);
+    uint64_t rb = 0;  // D16: the range guard of the fp16 stores
     float z[4][kHeadsMaxJ];
 #pragma unroll
     for (int g = 0; g < 4; g++) {
@@ -858,7 +867,13 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz,
             for (int j = 0; j < kHeadsMaxJ; j++) x = fmaf(z[g][j], sw[j][col], x);
             if (!((b[bit >> 5] >> (bit & 31)) & 1u)) x = 0.f;
             if (row < M && col < N) {
-                dy[(size_t)row * N + col] = x;
+                if constexpr (D16) {
+                    const _Float16 h = (_Float16)(x * oscale);
+                    range_val<P_F16>(rb, (float)h);
+                    reinterpret_cast<_Float16*>(dy)[(size_t)row * N + col] = h;
+                } else {
+                    dy[(size_t)row * N + col] = x;
+                }
                 cs += x;
             }
         }
@@ -866,6 +881,7 @@ __global__ __launch_bounds__(256) void k_heads_bwd(const float* __restrict__ dz,
         cs += __shfl_xor(cs, 32);
         if (lane < 16 && col < N) colsum[(size_t)rt * N + col] = cs;
     }
+    if constexpr (D16) range_note_wave<P_F16>(rb);
 }
 
 
@@ -1050,12 +1066,15 @@ __device__ __forceinline__ float wg_val16(uint32_t d, uint32_t sh, bool h16) {
 
 // XB: bytes per X element -- 4 (fp32) or 2 (fp16: P_F16's stored activations, and the heads' x3 weight
 // gradient over them; fp16 values are exact in fp32, so the staging is that of their fp32 values)
-template <int P, int TN, int NTK, int XB = 4>
+// AB: bytes per dY element -- 4, or 2 (P_F16's input gradients stored fp16 and pre-scaled: dscale 1)
+template <int P, int TN, int NTK, int XB = 4, int AB = 4>
 __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restrict__ dy, int lddy, float dscale,
                                                            const float* __restrict__ x, int ldx, int M, int N, int K,
                                                            int rows, int nslices, int ncb, float cscale,
                                                            float* __restrict__ ws) {
     static_assert(XB == 4 || (XB == 2 && P != P_X2), "fp16 X: P_F16 / P_X3");
+    static_assert(AB == 4 || (AB == 2 && P == P_F16), "fp16 dY: P_F16");
+    constexpr bool k16 = XB == 2 || AB == 2;  // some operand fp16: dword loads + half selects
     constexpr int kB = Prec<P>::kBlk;
     constexpr int np = Prec<P>::kPlanes;
     constexpr int RN = TN / kWgWaves;                               // n-tiles per wave in the rectangle
@@ -1072,7 +1091,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     if (s >= nslices) return;  // the whole workgroup
     const int m_begin = s * rows, nrows = min(M, m_begin + rows) - m_begin;
     const int col0 = cb * NTK * 16;
-    const float* const baseA = dy + (size_t)m_begin * lddy;
+    const void* const baseA = reinterpret_cast<const char*>(dy) + (size_t)m_begin * lddy * AB;
     const void* const baseB = reinterpret_cast<const char*>(x) + ((size_t)m_begin * ldx + col0) * XB;
 
     // loads through one buffer resource per piece slot q over the slice's rows (loop-invariant, built once),
@@ -1098,16 +1117,18 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
         // fp16 X (XB 2): every load is a dword (one instruction form for A and B slots, no branch between
         // load forms -- two forms merged at a branch made the compiler wait on each batch); the lane takes
         // the half (j & 1) of the dword holding its element (ldx even: rows stay dword-aligned)
-        voff[q] = ok ? (isA ? 4u * (uint32_t)(8 * c * lddy + j) : (uint32_t)XB * (uint32_t)(8 * c * ldx + j) & ~3u) : 0u;
-        hsh[q] = (!isA && XB == 2 && ok) ? 16u * (uint32_t)(j & 1) : 0u;
-        h16q[q] = !isA && XB == 2;  // per lane (from threadIdx, not readfirstlane): a select, not a branch
+        voff[q] = ok ? (isA ? (uint32_t)AB * (uint32_t)(8 * c * lddy + j) & ~3u
+                            : (uint32_t)XB * (uint32_t)(8 * c * ldx + j) & ~3u)
+                     : 0u;
+        h16q[q] = isA ? AB == 2 : XB == 2;  // per lane (from threadIdx, not readfirstlane): a select, not a branch
+        hsh[q] = (h16q[q] && ok) ? 16u * (uint32_t)(j & 1) : 0u;
         loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
         r8q[q] = 8 * c;
         // wave-uniform (itemsA = 64 TN), made scalar: a resource built from a divergent value becomes a
         // readfirstlane waterfall loop per load
         const bool isAu = __builtin_amdgcn_readfirstlane(threadIdx.x + kWgThreads * q) < itemsA;
         ldq[q] = isAu ? lddy : ldx;
-        eszq[q] = isAu ? 4u : (uint32_t)XB;
+        eszq[q] = isAu ? (uint32_t)AB : (uint32_t)XB;
         rsq[q] = __builtin_amdgcn_make_buffer_rsrc(isAu ? (void*)baseA : (void*)baseB, (short)0,
                                                    (int)(nrows * ldq[q] * eszq[q]), 0x00020000);
     }
@@ -1124,7 +1145,7 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     // i ld 4; x3 / f16 (VGPR room, and the scalar form spilled SGPRs in the f16 kernels -- a reloaded
     // spill is a fresh temporary, rewritten right after the load): one VGPR offset per (slot, row i),
     // each advanced in place.  tools/check_wgrad_operands.py checks the ISA of every instantiation.
-    constexpr bool kSOff = P == P_X2;
+    constexpr bool kSOff = P == P_X2;  // (x2 never has fp16 operands)
     constexpr int kNv = kSOff ? 1 : 8;
     uint32_t ob[kPer][kNv], sri[kPer][8];
 #pragma unroll
@@ -1214,8 +1235,8 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     auto store_piece_q = [&](int q, uint16_t* dst_set) {
         if (threadIdx.x + kWgThreads * q < items) {
             const bool isA = threadIdx.x + kWgThreads * q < itemsA;
-            if constexpr (XB == 2) {  // the fp16 halves of the loaded dwords, here where they are consumed (a
-                                      // conversion right after the load would wait for it there)
+            if constexpr (k16) {  // the fp16 halves of the loaded dwords, here where they are consumed (a
+                                  // conversion right after the load would wait for it there)
                 float v[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) v[i] = wg_val16(__float_as_uint(raw[q][i]), hsh[q], h16q[q]);
@@ -1615,7 +1636,7 @@ template <int P, int CT, int RT, int EM, int VW>
 __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restrict__ A, int lda, float ascale,
                                                    const uint16_t* __restrict__ B, int M, int N, int K, int nks,
                                                    BresPlan pl, Epi ep) {
-    static_assert(EM == EM_F32 || EM == EM_FWD || EM == EM_BWD || EM == EM_FWD16, "row-major outputs");
+    static_assert(EM == EM_F32 || em_fwd(EM) || em_bwd(EM), "row-major outputs");
     static_assert(VW != 16 || P == P_F16, "fp16 A: P_F16");
     constexpr int np = Prec<P>::kPlanes;
     extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
@@ -1649,7 +1670,7 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
             reinterpret_cast<uint2*>(sT + p * 256)[lane] = src[2 * lane];
         }
     }
-    if (EM != EM_BWD && ep.bias)
+    if (!em_bwd(EM) && ep.bias)
         for (int t = threadIdx.x; t < ctb * 16; t += 64 * kBresWaves) {
             const int col = 16 * t0 + t;
             sbias[t] = col < N ? ep.bias[col] : 0.f;
@@ -1670,7 +1691,7 @@ __global__ __launch_bounds__(64 * kBresWaves) void k_bres(const float* __restric
     const __amdgpu_buffer_rsrc_t arsrc =
         __builtin_amdgcn_make_buffer_rsrc((void*)A, (short)0, (int)((size_t)M * lda * aesz), 0x00020000);
     const __amdgpu_buffer_rsrc_t crs =  // C [M, ldc]: rows past M past num_records
-        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * (EM == EM_FWD16 ? 2 : 4)),
+        __builtin_amdgcn_make_buffer_rsrc((void*)ep.c, (short)0, (int)((size_t)M * ep.ldc * (em_16(EM) ? 2 : 4)),
                                           0x00020000);
     const __amdgpu_buffer_rsrc_t srs =  // colsum [ceil(M / 16), N]
         __builtin_amdgcn_make_buffer_rsrc((void*)ep.colsum, (short)0, (int)((size_t)((M + 15) / 16) * N * 4),
@@ -2060,8 +2081,10 @@ template <int P, int C, int VW>
 static int dispatch_bres_c(const float* a, int lda, float ascale, const uint16_t* b, int M, int N, int K,
                            const BresPlan& pl, const Epi& ep, hipStream_t s) {
     if (ep.c16) {
-        if constexpr (P == P_F16)
+        if constexpr (P == P_F16) {
             if (ep.mbits_out) return launch_bres<P, C, EM_FWD16, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+            if (ep.mbits_in) return launch_bres<P, C, EM_BWD16, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
+        }
         return MM_E_ARG;
     }
     if (ep.mbits_out) return launch_bres<P, C, EM_FWD, VW>(a, lda, ascale, b, M, N, K, pl, ep, s);
@@ -2100,14 +2123,14 @@ extern "C" int mm_x3_nt(const uint16_t* a_tp, const uint16_t* b_tp, int M, int N
     if (!a_tp || ((uintptr_t)a_tp & 15)) return MM_E_ARG;
     if (M == 0) return 0;
     Epi ep{bias, mask, nullptr, nullptr, c, c_tp, nullptr, ldc, ldm, relu, rup(N, 32) / 32, 1.f,
-           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31), 0};
+           c && (size_t)(M + 16) * ldc * 4 < ((size_t)1 << 31), 0, 1.f};
     return dispatch_nt<P_X3, ASrcTP>(a_tp, 0, 1.f, b_tp, M, N, K, ep, (hipStream_t)stream);
 }
 
 static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const uint16_t* b_tp, int M, int N, int K,
                         const float* bias, int relu, const float* mask, int ldm, const uint32_t* mbits_in,
                         uint32_t* mbits_out, float* colsum, float cscale, float* c, int ldc, uint16_t* c_tp,
-                        void* stream, int flags = 0) {
+                        void* stream, int flags = 0, float oscale = 1.f) {
     int e = check_common(b_tp, M, N, K, mask, ldm, c, ldc, c_tp);
     if (e) return e;
     if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
@@ -2116,7 +2139,7 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
     // fp16 activations (P_F16 only): A fp16 at scale 1 on the B-resident kernel; C fp16 for the forward with bits
     if ((a16 || c16) && (prec != MM_PREC_F16 || mask || c_tp)) return MM_E_ARG;
     if (a16 && (ascale != 1.f || (K & 3) || (lda & 3) || ((uintptr_t)a & 7))) return MM_E_ARG;
-    if (c16 && (!mbits_out || ((uintptr_t)c & 1))) return MM_E_ARG;
+    if (c16 && ((!mbits_out && !mbits_in) || ((uintptr_t)c & 1))) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (ascale != 1.f || cscale != 1.f)) return MM_E_ARG;  // the split is exact: no scaling
     const bool v4 = !a16 && !(K & 3) && !(lda & 3) && !((uintptr_t)a & 15);
     const bool v2 = !a16 && !(K & 1) && !(lda & 1) && !((uintptr_t)a & 7);
@@ -2140,19 +2163,22 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
                                         mask ? mask + m0 * ldm : nullptr, ldm,
                                         mbits_in ? mbits_in + rt0 * 64 * kMaskWords : nullptr,
                                         mbits_out ? mbits_out + rt0 * 64 * kMaskWords : nullptr,
-                                        colsum ? colsum + rt0 * N : nullptr, cscale, cm, ldc, nullptr, stream, flags);
+                                        colsum ? colsum + rt0 * N : nullptr, cscale, cm, ldc, nullptr, stream, flags,
+                                        oscale);
             if (rc) return rc;
         }
         return 0;
     }
     Epi ep{bias, mask, mbits_in, mbits_out, c, c_tp, colsum, ldc, ldm, relu, rup(N, 32) / 32, cscale, c != nullptr,
-           c16 ? 1 : 0};
+           c16 ? 1 : 0, oscale};
     hipStream_t s = (hipStream_t)stream;
     BresPlan pl;
     int cfg = C_NARROW;
-    if (a16) {  // fp16 A: the B-resident kernel only
+    if (a16 || (c16 && mbits_in)) {  // fp16 A, or fp16 input gradients: the B-resident kernel only
         if (!bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) return MM_E_ARG;
-        return dispatch_bres<P_F16, 16>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s);
+        return a16 ? dispatch_bres<P_F16, 16>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s)
+                   : (v4 ? dispatch_bres<P_F16, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s)
+                         : dispatch_bres<P_F16, 2>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s));
     }
     if (!mask && !c_tp && bres_enabled() && bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) {
         if (prec == MM_PREC_X3)
@@ -2194,15 +2220,28 @@ extern "C" int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const
 
 extern "C" int mm_gemm_nt_h(int prec, int flags, const void* a, int lda, float ascale, const uint16_t* b_tp, int M,
                             int N, int K, const float* bias, int relu, const uint32_t* mbits_in, uint32_t* mbits_out,
-                            float* colsum, float cscale, void* c, int ldc, void* stream) {
+                            float* colsum, float cscale, float oscale, void* c, int ldc, void* stream) {
     if (!c) return MM_E_ARG;
     return gemm_nt_f32a(prec, static_cast<const float*>(a), lda, ascale, b_tp, M, N, K, bias, relu, nullptr, 0,
-                        mbits_in, mbits_out, colsum, cscale, static_cast<float*>(c), ldc, nullptr, stream, flags);
+                        mbits_in, mbits_out, colsum, cscale, static_cast<float*>(c), ldc, nullptr, stream, flags,
+                        oscale);
 }
 
 // dY = (dz W) * bits (the heads' backward through the last ReLU, bits from the
 // last forward GEMM's mbits_out, N <= 272, J <= 8), and the per-16-row-tile
 // column sums colsum [ceil(M / 16), N].
+// the same with dY fp16 = fp16(dY * oscale) (P_F16's pre-scaled input gradients)
+extern "C" int mm_x3_heads_bwd_h16(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N,
+                                   void* dy, float* colsum, float oscale, void* stream) {
+    if (!dz || !W || !bits || !dy || !colsum || J <= 0 || J > kHeadsMaxJ || N <= 0 || N > 272 || M < 0)
+        return MM_E_ARG;
+    if (M == 0) return 0;
+    const int nrt = (M + 15) / 16;
+    hipLaunchKernelGGL((k_heads_bwd<17, true>), dim3((nrt + 3) / 4), dim3(256), 0, (hipStream_t)stream, dz, J, W, bits,
+                       M, N, static_cast<float*>(dy), colsum, oscale);
+    return (int)hipGetLastError();
+}
+
 extern "C" int mm_x3_heads_bwd(const float* dz, int J, const float* W, const uint32_t* bits, int M, int N, float* dy,
                                float* colsum, void* stream) {
     if (!dz || !W || !bits || !dy || !colsum || J <= 0 || J > kHeadsMaxJ || N <= 0 || N > 272 || M < 0)
@@ -2300,44 +2339,48 @@ static int launch_wgrad(const WgPlan& p, const float* dy, int lddy, float dscale
 }
 
 // the structured kernel for the (TN, NTK) blocks the actor and critic produce; 1 = no instantiation
-template <int P, int TN, int NTK, int XB = 4>
+template <int P, int TN, int NTK, int XB = 4, int AB = 4>
 static int launch_rect_t(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
                          int N, int K, float cscale, float* ws, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)k_wgrad_rect<P, TN, NTK, XB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess)
+        if (hipFuncSetAttribute((const void*)k_wgrad_rect<P, TN, NTK, XB, AB>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
             return MM_E_ARG;
         attr = true;
     }
     const size_t lds = (size_t)2 * (TN + NTK) * Prec<P>::kBlk * sizeof(uint16_t);
-    hipLaunchKernelGGL((k_wgrad_rect<P, TN, NTK, XB>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s, dy,
-                       lddy, dscale, x, ldx, M, N, K, p.rows, p.nslices, p.ncb, cscale, ws);
+    hipLaunchKernelGGL((k_wgrad_rect<P, TN, NTK, XB, AB>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s,
+                       dy, lddy, dscale, x, ldx, M, N, K, p.rows, p.nslices, p.ncb, cscale, ws);
     return (int)hipGetLastError();
 }
 
-template <int P, int XB = 4>
+template <int P, int XB = 4, int AB = 4>
 static int launch_rect_p(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
                          int N, int K, float cscale, float* ws, hipStream_t s) {
 #define MM_WR(a, b)                                                                                              \
     if (p.TN == a && p.NTK == b)                                                                                 \
-        return launch_rect_t<P, a, b, XB>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+        return launch_rect_t<P, a, b, XB, AB>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
     if constexpr (XB == 2 && P == P_X3) {  // fp16 X at x3: the actor heads' weight gradient over h3 only
         MM_WR(1, 17)
     } else {
         MM_WR(17, 9) MM_WR(17, 8) MM_WR(1, 17) MM_WR(4, 9) MM_WR(4, 4) MM_WR(1, 4)
     }
 #undef MM_WR
-    return XB == 2 ? MM_E_ARG : 1;  // fp16 X: no generic-kernel fallback
+    return (XB == 2 || AB == 2) ? MM_E_ARG : 1;  // fp16 operands: no generic-kernel fallback
 }
 
 static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int lddy, float dscale, const float* x,
-                             int ldx, int M, int N, int K, float cscale, float* ws, hipStream_t s, bool x16 = false) {
-    if (x16) {  // fp16 X (P_F16 / P_X3): the structured kernel only
-        if ((size_t)M * lddy * 4 >= ((size_t)1 << 31) || (size_t)M * ldx * 2 >= ((size_t)1 << 31)) return MM_E_ARG;
-        return prec == MM_PREC_X3    ? launch_rect_p<P_X3, 2>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
-               : prec == MM_PREC_F16 ? launch_rect_p<P_F16, 2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s)
-                                     : MM_E_ARG;
+                             int ldx, int M, int N, int K, float cscale, float* ws, hipStream_t s, bool x16 = false,
+                             bool a16 = false) {
+    if (x16 || a16) {  // fp16 operands (X: P_F16 / P_X3; dY: P_F16): the structured kernel only
+        if ((size_t)M * lddy * 4 >= ((size_t)1 << 31) || (size_t)M * ldx * 4 >= ((size_t)1 << 31)) return MM_E_ARG;
+        if ((x16 && (ldx & 1)) || (a16 && (lddy & 1))) return MM_E_ARG;  // fp16 rows: dword-aligned
+        if (prec == MM_PREC_X3) return a16 ? MM_E_ARG : launch_rect_p<P_X3, 2>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s);
+        if (prec != MM_PREC_F16) return MM_E_ARG;
+        if (a16 && x16) return launch_rect_p<P_F16, 2, 2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+        if (a16) return launch_rect_p<P_F16, 4, 2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+        return launch_rect_p<P_F16, 2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
     }
 #ifdef WG_GENERIC  // diagnostic builds: the generic kernel for every shape
     return 1;
@@ -2352,8 +2395,8 @@ static int launch_wgrad_rect(int prec, const WgPlan& p, const float* dy, int ldd
 static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
                       float cscale, float* ws, float* dw, void* stream, int flags = 0) {
     if (M < 0 || N <= 0 || K <= 0 || N > 16 * kWgMaxT || lddy < N || ldx < K) return MM_E_ARG;
-    if (flags & ~MM_GEMM_B_F16) return MM_E_ARG;
-    const bool x16 = flags & MM_GEMM_B_F16;
+    if (flags & ~(MM_GEMM_B_F16 | MM_GEMM_A_F16)) return MM_E_ARG;
+    const bool x16 = flags & MM_GEMM_B_F16, a16 = flags & MM_GEMM_A_F16;  // a16: dY fp16 (pre-scaled)
     if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return MM_E_ARG;
     if (prec == MM_PREC_X3 && (dscale != 1.f || cscale != 1.f)) return MM_E_ARG;
     hipStream_t s = (hipStream_t)stream;
@@ -2361,8 +2404,8 @@ static int gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const f
     if (!dy || !x || !ws) return MM_E_ARG;
     const WgPlan p = wg_plan(prec, M, N, K);
     if (!p.TPW) return MM_E_ARG;
-    int e = launch_wgrad_rect(prec, p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s, x16);
-    if (e == 1 && !x16)
+    int e = launch_wgrad_rect(prec, p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s, x16, a16);
+    if (e == 1 && !x16 && !a16)
         e = prec == MM_PREC_X3   ? launch_wgrad<P_X3>(p, dy, lddy, 1.f, x, ldx, M, N, K, 1.f, ws, s)
             : prec == MM_PREC_X2 ? launch_wgrad<P_X2>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s)
                                  : launch_wgrad<P_F16>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);

@@ -215,10 +215,13 @@ def _grad_scale(M, prec):
 
 
 def _wgrad(dy, x, prec, out=None):
-    """dW = dY^T X (mm_gemm_wgrad)."""
+    """dW = dY^T X (mm_gemm_wgrad).  An fp16 dY is the f16 networks' pre-scaled input gradient."""
     from . import x3
 
-    return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=_grad_scale(dy.shape[0], prec), out=out)
+    s = _grad_scale(dy.shape[0], prec)
+    if dy.dtype == torch.float16:
+        return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=1.0, cscale=1.0 / s, out=out)
+    return x3.wgrad(dy.contiguous(), x, prec=prec, dscale=s, out=out)
 
 
 # f16 networks: the update's hidden activations are stored in fp16 (mm_gemm_nt_h) -- every consumer rounds
@@ -259,23 +262,45 @@ def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None):
     """Backward through the ReLU layers given dY of the last one (already through
     its ReLU) and that dY's per-tile column sums cs (None: sum dY itself).
     outs: destinations [dW0, db0, dW1, db1, ...] (or None: allocated).
+    An fp16 dY is the f16 networks' pre-scaled input gradient (fp16(dY s), see
+    _g16): the layers' input gradients then stay fp16 pre-scaled too.
     Returns (dx or None, [dW0, db0, dW1, db1, ...])."""
     from . import x3
 
     L = len(ws)
-    s = _grad_scale(dy.shape[0], prec)
+    M = dy.shape[0]
+    s = _grad_scale(M, prec)
+    g16 = dy.dtype == torch.float16
     grads = [None] * (2 * L)
     dx = None
     for l in range(L - 1, -1, -1):
         o_w, o_b = (outs[2 * l], outs[2 * l + 1]) if outs is not None else (None, None)
         grads[2 * l] = _wgrad(dy, hs[l], prec, out=o_w)
+        assert cs is not None or not g16, "an fp16 dY comes with its column sums"
         grads[2 * l + 1] = x3.colsum(dy if cs is None else cs, out=o_b)
+        wt = x3.pack(ws[l], trans=True, prec=prec)
+        # pre-scaled fp16 dY: read at scale 1, the output unscaled by 1 / s (and stored fp16(. s) again)
+        ascale, cscale = (1.0, 1.0 / s) if g16 else (s, None)
         if l > 0:  # dY of layer l-1 = (dY W) * (h_l > 0): the ReLU bits of layer l-1's forward
-            cs = x3.colsum_buf(dy.shape[0], ws[l].shape[1], dy.device)
-            dy = x3.gemm(dy, x3.pack(ws[l], trans=True, prec=prec), mbits_in=ctx_bits[l - 1], colsum=cs, ascale=s)
+            cs = x3.colsum_buf(M, ws[l].shape[1], dy.device)
+            out = torch.empty((M, ws[l].shape[1]), dtype=torch.float16, device=dy.device) if g16 else None
+            dy = x3.gemm(dy, wt, mbits_in=ctx_bits[l - 1], colsum=cs, ascale=ascale, cscale=cscale, out=out,
+                         oscale=s)
         elif need_dx:
-            dx = x3.gemm(dy, x3.pack(ws[l], trans=True, prec=prec), ascale=s)
+            dx = x3.gemm(dy, wt, ascale=ascale, cscale=cscale)
     return dx, grads
+
+
+def _g16(prec, hs, ws, need_dx):
+    """fp16 pre-scaled input gradients (f16 with fp16 activations, F16_ACT): every input-gradient GEMM
+    takes fp16 A at its shape (the weight gradients take fp16 dY at the update's shapes)."""
+    from . import x3
+
+    M = hs[0].shape[0]
+    if prec != "f16" or hs[-1].dtype != torch.float16:
+        return False
+    shapes = [(w.shape[1], w.shape[0]) for w in ws[1:]] + ([(ws[0].shape[1], ws[0].shape[0])] if need_dx else [])
+    return all(n % 4 == 0 and k % 4 == 0 and x3.a16_ok(M, n, k) for n, k in shapes)
 
 
 def _heads_fwd(h, wh, bh):
@@ -303,13 +328,14 @@ def _heads_fwd(h, wh, bh):
     return out
 
 
-def _heads_bwd(dz, h, wh, bits, out_w=None, out_b=None):
-    """The heads' backward: (dY through the last ReLU, its tile column sums, dWh, dbh)."""
+def _heads_bwd(dz, h, wh, bits, out_w=None, out_b=None, oscale=None):
+    """The heads' backward: (dY through the last ReLU, its tile column sums, dWh, dbh).  oscale: dY
+    stored fp16 pre-scaled (fp16(dY oscale), see _g16)."""
     from . import x3
 
     dwh = _wgrad(dz, h, "x3", out=out_w)
     dbh = x3.colsum(dz, out=out_b)
-    dy, cs = x3.heads_bwd(dz, wh, bits)  # (dz Wh) * (h > 0), fp32
+    dy, cs = x3.heads_bwd(dz, wh, bits, oscale=oscale)  # (dz Wh) * (h > 0)
     return dy, cs, dwh, dbh
 
 
@@ -383,7 +409,8 @@ def _critic_bwd(hs, bits, params, dv, prec, outs=None):
     o = outs if outs is not None else [None] * 6
     dw2 = _wgrad(dv, hs[2], prec, out=o[4])
     db2 = x3.colsum(dv, out=o[5])
-    dy, cs = x3.heads_bwd(dv, w2, bits[1])  # (dV W2) * (h2 > 0)
+    g16 = _g16(prec, hs, (w0, w1), False)  # fp16 pre-scaled input gradients (f16 with fp16 activations)
+    dy, cs = x3.heads_bwd(dv, w2, bits[1], oscale=_grad_scale(dv.shape[0], prec) if g16 else None)
     _, grads = _mlp_bwd(bits, hs[:2], (w0, w1), dy, cs, prec, False, outs=o[:4] if outs is not None else None)
     return grads + [dw2, db2]
 
@@ -556,7 +583,10 @@ class Actor(nn.Module):
         w, _ = self.heads()
         gw = self._adjacent(_grad_of(self.move_head.weight), _grad_of(self.mark_head.weight))
         gb = self._adjacent(_grad_of(self.move_head.bias), _grad_of(self.mark_head.bias))
-        dy, cs, dwh, dbh = _heads_bwd(dz.contiguous(), hs[L], w, bits[L - 1], out_w=gw, out_b=gb)
+        params = self._mlp_params()
+        g16 = _g16(self.gemm_prec, hs, params[0::2], True)
+        dy, cs, dwh, dbh = _heads_bwd(dz.contiguous(), hs[L], w, bits[L - 1], out_w=gw, out_b=gb,
+                                      oscale=_grad_scale(dz.shape[0], self.gemm_prec) if g16 else None)
         if gw is None:
             self.move_head.weight.grad.copy_(dwh[:5])
             self.mark_head.weight.grad.copy_(dwh[5:])

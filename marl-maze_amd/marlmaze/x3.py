@@ -187,12 +187,14 @@ class deferred:
 
 
 def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None, ascale=1.0, out=None,
-         checked=False):
+         checked=False, cscale=None, oscale=1.0):
     """out = (1/ascale) ((ascale A) B^T) (+bias)(ReLU) in B's precision (mm_gemm_nt):
     A fp32 [M, K] row-major (16-byte rows, or 8-byte rows for N <= 64), B = TP
     [N, K].  mbits_out records the ReLU mask; mbits_in applies one (the input
     gradient through the ReLU below) with colsum its per-tile column sums.
-    ascale: a power of two for fp16 operands (1 for x3).
+    ascale: a power of two for fp16 operands (1 for x3); cscale (default 1 / ascale): the output's scale.
+    fp16 a / out (f16 only, mm_gemm_nt_h): the f16 networks' stored activations and pre-scaled input gradients
+    (an fp16 input-gradient out holds fp16(out * oscale)).
     checked (x2 / f16): read the range flag after the call (a synchronisation) and, when an operand left
     the fp16 range, redo the GEMM at x3 from B's source tensor (pack() records it)."""
     if checked and b.prec != "x3":
@@ -213,11 +215,13 @@ def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None
         assert b.prec == "f16" and out.dtype in (torch.float32, torch.float16), (b.prec, out.dtype)
         flags = ((_lib.GEMM_A_F16 if a.dtype == torch.float16 else 0)
                  | (_lib.GEMM_C_F16 if out.dtype == torch.float16 else 0))
+        cs = 1.0 / float(ascale) if cscale is None else float(cscale)
         _lib.check(_lib.lib().mm_gemm_nt_h(PRECS[b.prec], flags, _lib.ptr(a), a.stride(0), float(ascale), b.ptr(),
                                            M, N, K, _lib.ptr(bias), int(relu), _lib.ptr(mbits_in),
-                                           _lib.ptr(mbits_out), _lib.ptr(colsum), 1.0 / float(ascale), _lib.ptr(out),
+                                           _lib.ptr(mbits_out), _lib.ptr(colsum), cs, float(oscale), _lib.ptr(out),
                                            out.stride(0), _lib.stream_ptr()), "mm_gemm_nt_h")
         return out
+    assert cscale is None or cscale == 1.0 / float(ascale), "cscale: fp16 operands only"
     _lib.check(_lib.lib().mm_gemm_nt(PRECS[b.prec], _lib.ptr(a), a.stride(0), float(ascale), b.ptr(), M, N, K,
                                      _lib.ptr(bias), int(relu), _lib.ptr(mbits_in), _lib.ptr(mbits_out),
                                      _lib.ptr(colsum), 1.0 / float(ascale), _lib.ptr(out), out.stride(0),
@@ -248,7 +252,7 @@ def set_algo(name):
     return {v: k for k, v in _lib.GEMM_ALGO.items()}[prev]
 
 
-def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
+def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False, cscale=None):
     """dW [N, K] = dY^T X summed over the M rows (mm_gemm_wgrad), dY [M, N] and
     X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two).
     Inside a ``deferred()`` scope with ``out`` given, the row-slice partials'
@@ -263,8 +267,11 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dy.stride(1) == 1 and x.stride(1) == 1
-    assert x.dtype in (torch.float32, torch.float16) and dy.dtype == torch.float32, (x.dtype, dy.dtype)
-    flags = _lib.GEMM_B_F16 if x.dtype == torch.float16 else 0  # fp16 X: f16 activations (x3 / f16 only)
+    assert x.dtype in (torch.float32, torch.float16) and dy.dtype in (torch.float32, torch.float16), (x.dtype, dy.dtype)
+    # fp16 X: f16 activations (x3 / f16); fp16 dY: f16's pre-scaled input gradients (dscale 1, cscale the inverse)
+    flags = ((_lib.GEMM_B_F16 if x.dtype == torch.float16 else 0)
+             | (_lib.GEMM_A_F16 if dy.dtype == torch.float16 else 0))
+    cs = 1.0 / float(dscale) if cscale is None else float(cscale)
     defer = bool(_DEFER) and out is not None and M > 0  # a result the caller reads now is never deferred
     if out is None:
         out = torch.empty((N, K), dtype=torch.float32, device=dy.device)
@@ -274,7 +281,7 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
         S = L.mm_gemm_wgrad_slices(PRECS[prec], M, N, K)
         _lib.check(S if S < 0 else 0, "mm_gemm_wgrad_slices")
         ws = torch.empty(S * N * K, dtype=torch.float32, device=dy.device)
-        args = (_lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M, N, K, 1.0 / float(dscale),
+        args = (_lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M, N, K, cs,
                 _lib.ptr(ws), _lib.stream_ptr())
         _lib.check(L.mm_gemm_wgrad_partials_h(PRECS[prec], flags, *args) if flags
                    else L.mm_gemm_wgrad_partials(PRECS[prec], *args), "mm_gemm_wgrad_partials")
@@ -283,7 +290,7 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False):
         d.keep += [ws, out]
         return out
     ws = torch.empty(max(1, L.mm_gemm_wgrad_ws_len(M, N, K)), dtype=torch.float32, device=dy.device)
-    args = (_lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M, N, K, 1.0 / float(dscale),
+    args = (_lib.ptr(dy), dy.stride(0), float(dscale), _lib.ptr(x), x.stride(0), M, N, K, cs,
             _lib.ptr(ws), _lib.ptr(out), _lib.stream_ptr())
     _lib.check(L.mm_gemm_wgrad_h(PRECS[prec], flags, *args) if flags else L.mm_gemm_wgrad(PRECS[prec], *args),
                "mm_gemm_wgrad")
@@ -355,13 +362,19 @@ def colsum(x, out=None, slabs=256):
     return out
 
 
-def heads_bwd(dz, w, bits):
-    """dY = (dz [M, J] @ w [J, N]) * bits, and its per-tile column sums."""
+def heads_bwd(dz, w, bits, oscale=None):
+    """dY = (dz [M, J] @ w [J, N]) * bits, and its per-tile column sums.  oscale: dY stored fp16 as
+    fp16(dY * oscale) (the f16 networks' pre-scaled input gradients, mm_x3_heads_bwd_h16)."""
     M, J = dz.shape
     N = w.shape[1]
     dz, w = dz.contiguous(), w.contiguous()
-    dy = torch.empty((M, N), dtype=torch.float32, device=dz.device)
     cs = colsum_buf(M, N, dz.device)
+    if oscale is not None:
+        dy = torch.empty((M, N), dtype=torch.float16, device=dz.device)
+        _lib.check(_lib.lib().mm_x3_heads_bwd_h16(_lib.ptr(dz), J, _lib.ptr(w), _lib.ptr(bits), M, N, _lib.ptr(dy),
+                                                  _lib.ptr(cs), float(oscale), _lib.stream_ptr()), "mm_x3_heads_bwd_h16")
+        return dy, cs
+    dy = torch.empty((M, N), dtype=torch.float32, device=dz.device)
     _lib.check(_lib.lib().mm_x3_heads_bwd(_lib.ptr(dz), J, _lib.ptr(w), _lib.ptr(bits), M, N, _lib.ptr(dy),
                                           _lib.ptr(cs), _lib.stream_ptr()), "mm_x3_heads_bwd")
     return dy, cs

@@ -83,3 +83,57 @@ def test_f16_train_forward_stores_fp16_and_matches_fp32_storage(monkeypatch):
     for h, h32 in zip(hs[1:], saved32[2][1:]):
         assert torch.equal(h, h32.half())
     assert torch.equal(z, z32) or (z - z32).abs().max() <= 2e-3 * z32.abs().max()
+
+
+# ---- the input gradients stored fp16 pre-scaled: fp16(dY s), read back at scale 1 ----
+
+S = networks._grad_scale(M, "f16")
+
+
+@pytest.mark.parametrize("N,K,bits", [(264, 264, True), (64, 64, True), (460, 264, False)])
+def test_dgrad_fp16_prescaled_equals_fp32(N, K, bits):
+    """gemm(fp16(dY s), W^T) at ascale 1, cscale 1/s, stored fp16(. s) == fp16(s * the fp32 path's output),
+    with the same ReLU mask and column sums (the MFMA operands are the same fp16 values either way)."""
+    g = torch.Generator(device="cuda").manual_seed(5 * N + K)
+    dy32 = torch.randn(M, K, device="cuda", generator=g) / M
+    dy16 = (dy32 * S).half()
+    dy32 = dy16.float() / S  # the fp32 path's dY, exactly the stored one unscaled
+    w = x3.pack(torch.randn(K, N, device="cuda", generator=g) * 0.1, trans=True, prec="f16")  # W [K, N]^T
+    if bits:
+        mb = x3.mbits(M, "cuda").zero_()
+        h = torch.randn(M, N, device="cuda", generator=g)
+        x3.gemm(torch.randn(M, 64, device="cuda", generator=g), x3.pack(torch.randn(N, 64, device="cuda"),
+                                                                      prec="f16"), relu=True, mbits_out=mb)
+        cs32, cs16 = x3.colsum_buf(M, N, "cuda"), x3.colsum_buf(M, N, "cuda")
+        o32 = x3.gemm(dy32, w, mbits_in=mb, colsum=cs32, ascale=S)
+        out = torch.empty(M, N, dtype=torch.float16, device="cuda")
+        o16 = x3.gemm(dy16, w, mbits_in=mb, colsum=cs16, ascale=1.0, cscale=1.0 / S, out=out, oscale=S)
+        assert torch.equal(o16, (o32 * S).half())
+        assert torch.equal(cs16, cs32)
+        del h
+    else:  # the plain first-layer form: fp32 out
+        o32 = x3.gemm(dy32, w, ascale=S)
+        o16 = x3.gemm(dy16, w, ascale=1.0, cscale=1.0 / S)
+        assert o16.dtype == torch.float32 and torch.equal(o16, o32)
+
+
+@pytest.mark.parametrize("N,K,x16", [(264, 264, True), (264, 460, False), (64, 64, True), (64, 130, False)])
+def test_wgrad_fp16_prescaled_dy_equals_fp32(N, K, x16):
+    g = torch.Generator(device="cuda").manual_seed(9 * N + K)
+    dy16 = (torch.randn(M, N, device="cuda", generator=g) / M * S).half()
+    x = _h16(M, K, g) if x16 else torch.randn(M, K, device="cuda", generator=g)
+    d16 = x3.wgrad(dy16, x, prec="f16", dscale=1.0, cscale=1.0 / S)
+    d32 = x3.wgrad(dy16.float() / S, x, prec="f16", dscale=S)
+    assert torch.equal(d16, d32)
+
+
+def test_heads_bwd_fp16_prescaled():
+    g = torch.Generator(device="cuda").manual_seed(13)
+    dz = torch.randn(M, 6, device="cuda", generator=g) / M
+    w = torch.randn(6, 264, device="cuda", generator=g) * 0.1
+    mb = x3.mbits(M, "cuda").zero_()
+    x3.gemm(torch.randn(M, 64, device="cuda", generator=g), x3.pack(torch.randn(264, 64, device="cuda"), prec="f16"),
+            relu=True, mbits_out=mb)
+    dy32, cs32 = x3.heads_bwd(dz, w, mb)
+    dy16, cs16 = x3.heads_bwd(dz, w, mb, oscale=S)
+    assert dy16.dtype == torch.float16 and torch.equal(dy16, (dy32 * S).half()) and torch.equal(cs16, cs32)

@@ -16,7 +16,7 @@ def test_wgrad_staging_operands_never_rewritten():
     r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_wgrad_operands.py")],
                        capture_output=True, text=True, timeout=600)
     lines = [l for l in r.stdout.splitlines() if "k_wgrad_rect" in l]
-    assert len(lines) == 25, r.stdout + r.stderr  # 3 precisions x 6 shapes + 7 with fp16 X
+    assert len(lines) == 37, r.stdout + r.stderr  # 3 precisions x 6 shapes + 19 with fp16 operands
     assert all("foreign writes 0" in l for l in lines), r.stdout
     assert all("operand regs   0" not in l for l in lines), r.stdout  # the pinned loads were found
     assert r.returncode == 0, r.stdout + r.stderr
