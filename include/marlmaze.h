@@ -353,6 +353,19 @@ int mm_gemm_wgrad_partials_h(int prec, int flags, const float* dy, int lddy, flo
 int mm_heads_fwd_h16(const void* h, int ldh, int K, const float* w, const float* b, int M, float* logits,
                      void* stream);
 
+/* The actor trunk's three ReLU layers (networks.py:35-36) in one launch, for
+ * the rollout's small row counts (BASELINE configs[1]: 8,192 rows per step,
+ * where each layer alone sits at its launch floor).  Replaces three mm_gemm_nt
+ * calls (bias, ReLU, no bits); the result is bit-identical to them.
+ * out [M, ldc] = relu(relu(relu(h0 W0^T + b0) W1^T + b1) W2^T + b2): h0 fp32
+ * [M, lda] (K0 and lda multiples of 4, 16-byte aligned, K0 <= 512), w_l TP
+ * packs of [N_l, K_l] in precision prec (K_1 = N0, K_2 = N1), N_l <= 272,
+ * b_l [N_l] or NULL.  mm_trunk3_ok: whether the shape is supported (1 / 0). */
+int mm_trunk3_ok(int prec, int M, int K0, int N0, int N1, int N2, int lda);
+int mm_trunk3(int prec, const float* h0, int lda, int M, int K0, const uint16_t* w0, const float* b0, int N0,
+              const uint16_t* w1, const float* b1, int N1, const uint16_t* w2, const float* b2, int N2, float* out,
+              int ldc, void* stream);
+
 /* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
  * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),
  * masks [2M, 6] u8, actions [2M, 2] i8 (move, mark); per sample the joint

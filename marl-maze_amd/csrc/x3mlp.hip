@@ -388,6 +388,34 @@ struct ASrcTP {  // pre-split TP planes: three lane-linear 1-KiB loads
     }
 };
 
+// a lane's 8 fp32 A values of one k-step (r[0]: k 4c..4c+3, r[1]: k 16+4c..: kcol order) -> its fragment
+// planes: split (P_X3), hi / lo pairs of x s (P_X2), or rounded after scaling (P_F16)
+template <int P>
+__device__ __forceinline__ void frag_f32(const float4 (&r)[2], float scale, bf16x8 (&a)[3]) {
+    if constexpr (P == P_X3) {
+        uint32_t h[4], m[4], l[4];
+        split2(r[0].x, r[0].y, h[0], m[0], l[0]);
+        split2(r[0].z, r[0].w, h[1], m[1], l[1]);
+        split2(r[1].x, r[1].y, h[2], m[2], l[2]);
+        split2(r[1].z, r[1].w, h[3], m[3], l[3]);
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+        a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
+        a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    } else if constexpr (P == P_X2) {
+        uint32_t h[4], l[4];
+        pair2(r[0].x, r[0].y, scale, h[0], l[0]);
+        pair2(r[0].z, r[0].w, scale, h[1], l[1]);
+        pair2(r[1].x, r[1].y, scale, h[2], l[2]);
+        pair2(r[1].z, r[1].w, scale, h[3], l[3]);
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+        a[1] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    } else {
+        const float s = scale;
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(f16x2_rn(r[0].x * s, r[0].y * s), f16x2_rn(r[0].z * s, r[0].w * s),
+                                                     f16x2_rn(r[1].x * s, r[1].y * s), f16x2_rn(r[1].z * s, r[1].w * s)));
+    }
+}
+
 // fp32 row-major [M, lda]: VW = 4 (16-byte loads; lda % 4 == 0) or 2 (8-byte
 // loads: lda, K even, e.g. the critic's [M, 130] observations), split (P_X3)
 // or rounded after scaling (P_F16) in registers
@@ -427,28 +455,7 @@ struct ASrcF32V {
     }
     template <int P>
     __device__ __forceinline__ void frag(const Raw& r, bf16x8 (&a)[3]) const {
-        if constexpr (P == P_X3) {
-            uint32_t h[4], m[4], l[4];
-            split2(r[0].x, r[0].y, h[0], m[0], l[0]);
-            split2(r[0].z, r[0].w, h[1], m[1], l[1]);
-            split2(r[1].x, r[1].y, h[2], m[2], l[2]);
-            split2(r[1].z, r[1].w, h[3], m[3], l[3]);
-            a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-            a[1] = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
-            a[2] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
-        } else if constexpr (P == P_X2) {
-            uint32_t h[4], l[4];
-            pair2(r[0].x, r[0].y, scale, h[0], l[0]);
-            pair2(r[0].z, r[0].w, scale, h[1], l[1]);
-            pair2(r[1].x, r[1].y, scale, h[2], l[2]);
-            pair2(r[1].z, r[1].w, scale, h[3], l[3]);
-            a[0] = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-            a[1] = __builtin_bit_cast(bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
-        } else {
-            const float s = scale;
-            a[0] = __builtin_bit_cast(bf16x8, make_uint4(f16x2_rn(r[0].x * s, r[0].y * s), f16x2_rn(r[0].z * s, r[0].w * s),
-                                                         f16x2_rn(r[1].x * s, r[1].y * s), f16x2_rn(r[1].z * s, r[1].w * s)));
-        }
+        frag_f32<P>(r, scale, a);
     }
 };
 typedef ASrcF32V<4> ASrcF32;
@@ -809,6 +816,323 @@ __global__ __launch_bounds__(SW<P>::kThreads) void k_x3nt(const AT* __restrict__
         X3_STAMP(it, 3, __builtin_amdgcn_s_memtime());
         X3_STAMP(it, 5, __builtin_amdgcn_s_memrealtime());
     }
+}
+
+// ---------------------------------------------------------------------------
+// The actor trunk's three ReLU layers in ONE launch for small M (the rollout's per-step forward at BASELINE
+// configs[1]: 4,096 mazes = 8,192 rows; networks.py:35-36 under torch.no_grad, PPO.py:170-186):
+//   h3 = relu(relu(relu(h0 W0^T + b0) W1^T + b1) W2^T + b2)
+// At that size each layer on k_x3nt is a chain of k-steps at its launch floor (~13.6 us each, 160
+// workgroups).  Here one workgroup owns 16 RT rows through all three layers.  The unit's h0 rows and each
+// hidden layer's output stay in LDS, already in the precision's fragment planes (TP order, converted ONCE:
+// h0 at staging, each hidden layer in its producer's epilogue), so a wave's A fragment is one lane-linear
+// ds_read_b128 per plane and no wave repeats another's conversion.  Wave w owns the column-tile pair
+// (2w, 2w + 1) -- one 32-column TP block of the output -- and tile 16 (N <= 272) is split by row tiles
+// over waves 0, 5, 2 (SIMDs 0, 1, 2: no SIMD carries a whole third tile); the weight
+// fragments come straight from the TP planes in L2 into registers, D k-steps ahead.  Only h0 is read from
+// HBM and only h3 written.  Bit-identical to three k_x3nt launches (EM_F32, ReLU): the same conversion of
+// the same fp32 values (store_piece = frag_f32 per value), the same MFMA sequence per output tile in k
+// order (mma), the same epilogue arithmetic.  The weight-fragment loads follow the k_wgrad_rect rule
+// (DESIGN.md section 4): their VGPR offsets are advanced in place and held live until consumed.
+// ---------------------------------------------------------------------------
+constexpr int kTrWaves = 8;
+constexpr int kTrMaxN = 272;   // 17 column tiles: pairs 0..7 to waves 0..7, tile 16's row tiles to waves 0, 5, 2
+constexpr int kTrMaxK0 = 512;  // padded width of the staged h0
+constexpr int kTrSlice = 16 * 36;  // floats: a wave's [16 rows][32 columns] epilogue slice (stride 36)
+struct TrunkArgs {
+    const float* h0;
+    const uint16_t* w[3];  // TP [N_l, K_l] in the precision P (K_1 = N_0, K_2 = N_1)
+    const float* b[3];     // [N_l] or null
+    float* out;            // fp32 [M, ldc]
+    int lda, ldc, M, K0;
+    int N[3];
+    int bx;  // uint16 offset of the second activation buffer (bufH) from the first (bufX)
+};
+
+#ifdef X3_STAMPS  // diagnostic builds only (tools/trunk_stamps.py): per-wave phase clocks of k_trunk3
+__device__ unsigned long long g_tr_stamps[1024 * kTrWaves * 10];
+#define TR_STAMP(slot, val)                                                                      \
+    do {                                                                                         \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024)                                        \
+            g_tr_stamps[(blockIdx.x * kTrWaves + (threadIdx.x >> 6)) * 10 + (slot)] = (val);     \
+    } while (0)
+#else
+#define TR_STAMP(slot, val) \
+    do {                    \
+    } while (0)
+#endif
+
+// the column tile of a wave's accumulator slot c: 2 w, 2 w + 1, then 16 (one row tile of it, on waves 0, 5, 2)
+__device__ __forceinline__ int trunk_tile(int wave, int c) { return c < 2 ? 2 * wave + c : 16; }
+// the row tile of tile 16 on wave w (-1: none)
+__device__ __forceinline__ int trunk_r16(int w) { return w == 0 ? 0 : w == 5 ? 1 : w == 2 ? 2 : -1; }
+
+// one layer: dst = relu(src W^T + b) for the unit's 16 RT rows.  src: TP blocks (rt, ks) of the layer
+// input in LDS (nks = ceil(K / 32) per row tile); dst: the same for the output (dstL), or the global output
+// rows (dstL null).  NC: the wave's tiles; D: the weight prefetch depth in k-steps, nks % D == 0 -- both
+// compile-time, and the k-loop is branch-free (groups of D steps, the last one peeled): branches in it made
+// the compiler's wait counting fall back to waiting for every load in flight at each step.
+template <int P, int RT, int D, int NC>
+__device__ __forceinline__ void trunk_layer_n(const uint16_t* src, int K, const uint16_t* W, int N, const float* sb,
+                                              uint16_t* dstL, float* slice, const TrunkArgs& ta, int m0, int wave,
+                                              int lane, uint32_t& rm, int stamp) {
+    constexpr int np = Prec<P>::kPlanes;
+    constexpr uint32_t kBS = 2u * Prec<P>::kBlk;  // bytes per TP block (16 rows x 32 k, all planes)
+    const int nks = rup(K, 32) / 32, tiles = (N + 15) / 16;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)W, (short)0, (int)((uint32_t)tiles * nks * kBS), 0x00020000);
+    // slot s holds the fragments of the k-steps s, s + D, ...; ob[s][c]: the lane's byte offset of its
+    // fragment piece in block (tile, next k-step of the slot), advanced in place after each use
+    uint32_t ob[D][NC];
+#pragma unroll
+    for (int s = 0; s < D; s++)
+#pragma unroll
+        for (int c = 0; c < NC; c++) ob[s][c] = ((uint32_t)trunk_tile(wave, c) * nks + s) * kBS + 16u * lane;
+    bf16x8 bq[D][NC][3];
+    auto issue = [&](int s) {
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int p = 0; p < np; p++)
+                bq[s][c][p] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, ob[s][c] + 1024u * p, 0, 0));
+    };
+    auto advance = [&](int s) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int c = 0; c < NC; c++) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[s][c]) : "s"((uint32_t)D * kBS));
+    };
+    const bf16x8* const a8 = reinterpret_cast<const bf16x8*>(src) + lane;
+    f32x4 acc[NC][RT], accx[NC][RT];
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++) acc[c][rt] = accx[c][rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // slot 2 (tile 16) covers one row tile r2 (trunk_r16); its A fragment picked by per-lane selects (from
+    // threadIdx, not the wave-uniform value: a uniform select became a branch)
+    static_assert(RT <= 3, "tile 16's row tiles: waves 0, 5, 2");
+    const int r2 = trunk_r16(wave);
+    const int r2v = trunk_r16((int)(threadIdx.x >> 6));
+    // A fragments one k-step ahead (the last step re-reads its own block: no branch in the loop)
+    bf16x8 an[RT][3];
+    auto load_a = [&](int ks) {
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int q = 0; q < np; q++) an[rt][q] = a8[((rt * nks + ks) * np + q) * 64];
+    };
+    load_a(0);
+    auto compute = [&](int ks, int s) {
+        bf16x8 a[RT][3];
+#pragma unroll
+        for (int rt = 0; rt < RT; rt++)
+#pragma unroll
+            for (int q = 0; q < np; q++) a[rt][q] = an[rt][q];
+        load_a(min(ks + 1, nks - 1));
+#pragma unroll
+        for (int c = 0; c < (NC < 2 ? NC : 2); c++)
+#pragma unroll
+            for (int rt = 0; rt < RT; rt++) acc[c][rt] = mma<P>(a[rt], bq[s][c], acc[c][rt], accx[c][rt]);
+        if constexpr (NC == 3) {
+            bf16x8 a2[3];
+#pragma unroll
+            for (int q = 0; q < np; q++) {
+                a2[q] = a[0][q];
+#pragma unroll
+                for (int rt = 1; rt < RT; rt++) a2[q] = r2v == rt ? a[rt][q] : a2[q];
+            }
+            acc[2][0] = mma<P>(a2, bq[s][2], acc[2][0], accx[2][0]);
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < D; s++) issue(s);
+    const int G = nks / D;
+    for (int g = 0; g + 1 < G; g++) {
+#pragma unroll
+        for (int s = 0; s < D; s++) {
+            compute(g * D + s, s);
+            advance(s);
+            issue(s);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < D; s++) compute((G - 1) * D + s, s);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < D; s++)
+#pragma unroll
+        for (int c = 0; c < NC; c++) asm volatile("" ::"v"(ob[s][c]));  // held to here (all loads consumed)
+    TR_STAMP(stamp, __builtin_amdgcn_s_memtime());
+    (void)stamp;
+    // epilogue: the k_x3nt arithmetic (x2_combine; cscale 1; + bias; ReLU)
+    const int rq = 4 * (lane >> 4);
+    float x[NC][RT][4];
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const float bv = sb[16 * trunk_tile(wave, c) + (lane & 15)];
+#pragma unroll
+        for (int rt = 0; rt < (c < 2 ? RT : 1); rt++) {
+            const f32x4 v = x2_combine<P>(acc[c][rt], accx[c][rt]);
+            range_acc<P>(rm, v);
+#pragma unroll
+            for (int g = 0; g < 4; g++) x[c][rt][g] = fmaxf(v[g] + bv, 0.f);
+        }
+    }
+    if (!dstL) {  // the last layer: fp32 rows of the output (16 lanes: 64 contiguous bytes of a row)
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            const int col = 16 * trunk_tile(wave, c) + (lane & 15);
+#pragma unroll
+            for (int rt = 0; rt < (c < 2 ? RT : 1); rt++)
+#pragma unroll
+                for (int g = 0; g < 4; g++) {
+                    const int row = m0 + 16 * (c < 2 ? rt : r2) + rq + g;
+                    if (row < ta.M && col < N) ta.out[(size_t)row * ta.ldc + col] = x[c][rt][g];
+                }
+        }
+        return;
+    }
+    // a hidden layer: each owned 32-column block (tile pair) through an fp32 slice into fragment order,
+    // converted once (store_piece), into the next layer's input blocks; a missing tile of a pair is zeros.
+    // x2 / x3: the slice is the destination block itself (2 KiB of fp32 fit its np KiB; the block is this
+    // wave's until the layer's barrier), 32 floats a row with the float4 groups XOR-swizzled by row / 2 (a
+    // 16-row column read then touches distinct banks); f16: the wave's own slice (rows of 36 floats).
+    const int nksD = rup(N, 32) / 32, rr = lane & 15, ch = lane >> 4;
+    auto sidx = [&](int row, int col) {
+        return np >= 2 ? row * 32 + ((((col >> 2) ^ ((row >> 1) & 7))) << 2) + (col & 3) : row * 36 + col;
+    };
+    // slots c0, c1 (-1: no tile) of the wave's row tile rs -> block (rt, ks)
+    auto put_block = [&](int ks, int rt, int rs, int c0, int c1) {
+        uint16_t* const blk = dstL + (size_t)(rt * nksD + ks) * np * 512;
+        float* const sl = np >= 2 ? reinterpret_cast<float*>(blk) : slice;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            sl[sidx(rq + g, lane & 15)] = c0 >= 0 ? x[c0 >= 0 ? c0 : 0][rs][g] : 0.f;
+            sl[sidx(rq + g, 16 + (lane & 15))] = c1 >= 0 ? x[c1 >= 0 ? c1 : 0][rs][g] : 0.f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const float4 v0 = *reinterpret_cast<const float4*>(sl + sidx(rr, kcol(ch, 0)));
+        const float4 v1 = *reinterpret_cast<const float4*>(sl + sidx(rr, kcol(ch, 4)));
+        const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // (in place: every lane has read the block before it is overwritten)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        store_piece<P>(v, 1.f, reinterpret_cast<uint4*>(blk) + lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the slice is rewritten next
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+#pragma unroll
+    for (int rt = 0; rt < RT; rt++)
+        if (NC >= 1) put_block(wave, rt, rt, 0, NC >= 2 ? 1 : -1);
+    if (NC >= 3) put_block(8, r2, 0, 2, -1);
+    (void)nksD;
+}
+
+template <int P, int RT, int D>
+__device__ __forceinline__ void trunk_layer(const uint16_t* src, int K, const uint16_t* W, int N, const float* sb,
+                                            uint16_t* dstL, float* slice, const TrunkArgs& ta, int m0, int wave,
+                                            int lane, uint32_t& rm, int stamp) {
+    const int tiles = (N + 15) / 16, nks = rup(K, 32) / 32;
+    // wave-uniform: slots 0, 1 = tiles 2 w, 2 w + 1; slot 2 = one row tile of tile 16 (N > 256)
+    const int nc = 2 * wave >= tiles ? 0 : 2 * wave + 1 >= tiles ? 1 : (trunk_r16(wave) >= 0 && trunk_r16(wave) < RT && tiles > 16) ? 3 : 2;
+    if (nks % D == 0) {
+        if (nc == 3) trunk_layer_n<P, RT, D, 3>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 2) trunk_layer_n<P, RT, D, 2>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 1) trunk_layer_n<P, RT, D, 1>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+    } else {  // (shapes other than the actor's: no prefetch beyond the next k-step)
+        if (nc == 3) trunk_layer_n<P, RT, 1, 3>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 2) trunk_layer_n<P, RT, 1, 2>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 1) trunk_layer_n<P, RT, 1, 1>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+    }
+}
+
+template <int P, int RT, int D>
+__global__ __launch_bounds__(64 * kTrWaves) void k_trunk3(TrunkArgs ta) {
+    constexpr int np = Prec<P>::kPlanes;
+    constexpr int kIt = (RT * (kTrMaxK0 / 32) * 64 + 64 * kTrWaves - 1) / (64 * kTrWaves);  // h0 pieces per thread (max)
+    extern __shared__ __attribute__((aligned(16))) float tls[];
+    float* const sbias = tls;                       // [3][kTrMaxN], zero past N
+    float* const slices = tls + 3 * kTrMaxN;        // f16: [waves][kTrSlice] (x2 / x3 convert in place)
+    uint16_t* const bufX = reinterpret_cast<uint16_t*>(slices + (np == 1 ? kTrWaves * kTrSlice : 0));  // h0, then layer 1's output
+    uint16_t* const bufH = bufX + ta.bx;                                                 // layer 0's output
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m0 = blockIdx.x * 16 * RT;
+    TR_STAMP(0, __builtin_amdgcn_s_memtime());
+    TR_STAMP(8, __builtin_amdgcn_s_memrealtime());
+    {  // the unit's h0 rows as TP blocks (zero past M and past K0 up to the 32-column padding): every load
+       // issued first, branch-free (out-of-range pieces read zeros through the buffer range check), their
+       // offsets held until the data is consumed (the k_wgrad_rect rule)
+        const int nks0 = rup(ta.K0, 32) / 32, npc = RT * nks0 * 64;
+        const int nrows = min(16 * RT, ta.M - m0);
+        const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(ta.h0 + (size_t)m0 * ta.lda), (short)0, (int)((uint32_t)nrows * ta.lda * 4u), 0x00020000);
+        uint32_t off[kIt][2];
+        float4 v[kIt][2];
+#pragma unroll
+        for (int j = 0; j < kIt; j++) {
+            const int i = threadIdx.x + 64 * kTrWaves * j, l = i & 63, blk = i >> 6;  // blk = rt nks0 + ks
+            const int rt = blk / nks0, ks = blk - nks0 * rt;
+            const int row = 16 * rt + (l & 15), k0 = 32 * ks + 4 * (l >> 4);
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+                off[j][h] = (i < npc && row < nrows && k0 + 16 * h < ta.K0) ? 4u * ((uint32_t)row * ta.lda + k0 + 16 * h)
+                                                                           : kBufOOB;
+        }
+#pragma unroll
+        for (int j = 0; j < kIt; j++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const u32x4v d = __builtin_amdgcn_raw_buffer_load_b128(hrs, off[j][h], 0, 0);
+                v[j][h] = make_float4(__uint_as_float(d.x), __uint_as_float(d.y), __uint_as_float(d.z),
+                                      __uint_as_float(d.w));
+            }
+        // the biases: thread t < 272 loads column t of each layer's (zero past N_l, or for a null bias), in
+        // flight together with h0
+        const uint32_t boff = 4u * threadIdx.x;
+        float bv[3];
+#pragma unroll
+        for (int l = 0; l < 3; l++) {
+            const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)ta.b[l], (short)0, ta.b[l] ? 4 * ta.N[l] : 0, 0x00020000);
+            bv[l] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, boff, 0, 0));
+        }
+        if (threadIdx.x < kTrMaxN) {
+#pragma unroll
+            for (int l = 0; l < 3; l++) sbias[kTrMaxN * l + threadIdx.x] = bv[l];
+        }
+        asm volatile("" ::"v"(boff));
+#pragma unroll
+        for (int j = 0; j < kIt; j++) {
+            const int i = threadIdx.x + 64 * kTrWaves * j;
+            if (i < npc) {
+                const float e[8] = {v[j][0].x, v[j][0].y, v[j][0].z, v[j][0].w, v[j][1].x, v[j][1].y, v[j][1].z, v[j][1].w};
+                store_piece<P>(e, 1.f, reinterpret_cast<uint4*>(bufX + (size_t)(i >> 6) * np * 512) + (i & 63));
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < kIt; j++)
+#pragma unroll
+            for (int h = 0; h < 2; h++) asm volatile("" ::"v"(off[j][h]));
+    }
+    __syncthreads();
+    TR_STAMP(1, __builtin_amdgcn_s_memtime());
+    float* const slice = slices + wave * kTrSlice;
+    uint32_t rm = 0;  // the range guard (range_acc)
+    trunk_layer<P, RT, D>(bufX, ta.K0, ta.w[0], ta.N[0], sbias, bufH, slice, ta, m0, wave, lane, rm, 2);
+    __syncthreads();
+    TR_STAMP(3, __builtin_amdgcn_s_memtime());
+    trunk_layer<P, RT, D>(bufH, ta.N[0], ta.w[1], ta.N[1], sbias + kTrMaxN, bufX, slice, ta, m0, wave, lane, rm, 4);
+    __syncthreads();
+    TR_STAMP(5, __builtin_amdgcn_s_memtime());
+    trunk_layer<P, RT, D>(bufX, ta.N[1], ta.w[2], ta.N[2], sbias + 2 * kTrMaxN, nullptr, slice, ta, m0, wave, lane, rm,
+                          6);
+    range_note<P>(rm);
+    TR_STAMP(7, __builtin_amdgcn_s_memtime());
+    TR_STAMP(9, __builtin_amdgcn_s_memrealtime());
 }
 
 // Backward of the actor heads into the last hidden layer (networks.py:38-41 +
@@ -1793,6 +2117,11 @@ extern "C" int mm_x3_stamps_read(unsigned long long* out, long n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_stamps), (n < cap ? n : cap) * sizeof(unsigned long long), 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
+extern "C" int mm_trunk_stamps_read(unsigned long long* out, long n) {
+    const long cap = (long)(sizeof(g_tr_stamps) / sizeof(g_tr_stamps[0]));
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tr_stamps), (n < cap ? n : cap) * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
 extern "C" int mm_x3_stamps_clear() {
     static unsigned long long zero[256 * 16 * kWaves * 8];
     return hipMemcpyToSymbol(HIP_SYMBOL(g_x3_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice) == hipSuccess
@@ -2225,6 +2554,80 @@ extern "C" int mm_gemm_nt_h(int prec, int flags, const void* a, int lda, float a
     return gemm_nt_f32a(prec, static_cast<const float*>(a), lda, ascale, b_tp, M, N, K, bias, relu, nullptr, 0,
                         mbits_in, mbits_out, colsum, cscale, static_cast<float*>(c), ldc, nullptr, stream, flags,
                         oscale);
+}
+
+// ---- the fused small-M trunk (k_trunk3) ----
+// row tiles per workgroup: 2 (MARLMAZE_TRUNK_RT=3: 3 where the LDS holds them -- fewer workgroups
+// re-reading the weights from L2, but each one's k-loops 1.27x longer: 25.3 vs 22.3 us at 8,192 rows, x2).  Weight fragments D
+// k-steps ahead: 1 for x2 / x3, 3 for f16 (its k-steps are 3x shorter); MARLMAZE_TRUNK_D=1 or 3 forces one.
+static int trunk_env(const char* name) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : 0;
+}
+
+// LDS: the biases, the f16 kernels' epilogue slices, then two activation buffers of TP blocks (uint16):
+// bufX = h0 / layer 1's output, bufH = layer 0's output
+static void trunk_bufs(int prec, int RT, int K0, int N0, int N1, int& bx, size_t& lds) {
+    const int np = prec == MM_PREC_X3 ? 3 : prec == MM_PREC_X2 ? 2 : 1;
+    const int nx = std::max(rup(K0, 32), rup(N1, 32)) / 32, nh = rup(N0, 32) / 32;
+    bx = RT * nx * np * 512;
+    lds = (size_t)(3 * kTrMaxN + (np == 1 ? kTrWaves * kTrSlice : 0)) * 4 + (size_t)RT * (nx + nh) * np * 1024;
+}
+
+static int trunk_pick_rt(int prec, int K0, int N0, int N1) {
+    int bx;
+    size_t lds;
+    if (trunk_env("MARLMAZE_TRUNK_RT") == 3) {
+        trunk_bufs(prec, 3, K0, N0, N1, bx, lds);
+        if (lds <= 160 * 1024) return 3;
+    }
+    trunk_bufs(prec, 2, K0, N0, N1, bx, lds);
+    return lds <= 160 * 1024 ? 2 : 0;
+}
+
+extern "C" int mm_trunk3_ok(int prec, int M, int K0, int N0, int N1, int N2, int lda) {
+    if (prec != MM_PREC_X3 && prec != MM_PREC_F16 && prec != MM_PREC_X2) return 0;
+    if (M < 0 || K0 <= 0 || (K0 & 3) || (lda & 3) || lda < K0 || rup(K0, 32) > kTrMaxK0) return 0;
+    if (N0 <= 0 || N1 <= 0 || N2 <= 0 || N0 > kTrMaxN || N1 > kTrMaxN || N2 > kTrMaxN) return 0;
+    return trunk_pick_rt(prec, K0, N0, N1) ? 1 : 0;
+}
+
+template <int P, int RT, int D>
+static int launch_trunk(const TrunkArgs& ta, size_t lds, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k_trunk3<P, RT, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return MM_E_ARG;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_trunk3<P, RT, D>), dim3((ta.M + 16 * RT - 1) / (16 * RT)), dim3(64 * kTrWaves), lds, s, ta);
+    return (int)hipGetLastError();
+}
+
+template <int P>
+static int launch_trunk_p(TrunkArgs& ta, int RT, hipStream_t s) {
+    const int de = trunk_env("MARLMAZE_TRUNK_D");
+    const int d = de == 1 || de == 3 ? de : P == P_F16 ? 3 : 1;
+    size_t lds;
+    trunk_bufs(P, RT, ta.K0, ta.N[0], ta.N[1], ta.bx, lds);
+    if (RT == 3) return d == 3 ? launch_trunk<P, 3, 3>(ta, lds, s) : launch_trunk<P, 3, 1>(ta, lds, s);
+    return d == 3 ? launch_trunk<P, 2, 3>(ta, lds, s) : launch_trunk<P, 2, 1>(ta, lds, s);
+}
+
+extern "C" int mm_trunk3(int prec, const float* h0, int lda, int M, int K0, const uint16_t* w0, const float* b0,
+                         int N0, const uint16_t* w1, const float* b1, int N1, const uint16_t* w2, const float* b2,
+                         int N2, float* out, int ldc, void* stream) {
+    if (!mm_trunk3_ok(prec, M, K0, N0, N1, N2, lda) || !h0 || !out || !w0 || !w1 || !w2 || ldc < N2) return MM_E_ARG;
+    if (((uintptr_t)h0 & 15) || (((uintptr_t)w0 | (uintptr_t)w1 | (uintptr_t)w2) & 15) || ((uintptr_t)out & 3))
+        return MM_E_ARG;
+    if (M == 0) return 0;
+    TrunkArgs ta{h0, {w0, w1, w2}, {b0, b1, b2}, out, lda, ldc, M, K0, {N0, N1, N2}, 0};
+    const int RT = trunk_pick_rt(prec, K0, N0, N1);
+    hipStream_t s = (hipStream_t)stream;
+    if (prec == MM_PREC_X2) return launch_trunk_p<P_X2>(ta, RT, s);
+    if (prec == MM_PREC_F16) return launch_trunk_p<P_F16>(ta, RT, s);
+    return launch_trunk_p<P_X3>(ta, RT, s);
 }
 
 // dY = (dz W) * bits (the heads' backward through the last ReLU, bits from the

@@ -240,13 +240,24 @@ def _act16(prec, M, widths, next_ks):
             and all(x3.a16_ok(M, n, k) for n, k in next_ks))
 
 
+# three ReLU layers without bits (the rollout's trunk) up to this many rows run as ONE launch (mm_trunk3:
+# bit-identical to the per-layer GEMMs, which sit at their launch floor there); 0 switches it off
+TRUNK_MAX_ROWS = int(os.environ.get("MARLMAZE_TRUNK_MAX_ROWS", "16384"))
+
+
 def _mlp_fwd(h0, ws, bs, prec, need_bits, act16=False):
     """The ReLU layers on the engine; returns the activations [h0, h1, ...] and
     the forward GEMMs' ReLU bit masks (None without need_bits).  act16: the
-    layers' outputs in fp16 (f16 with bits only, see F16_ACT)."""
+    layers' outputs in fp16 (f16 with bits only, see F16_ACT).  Three layers
+    without bits at <= TRUNK_MAX_ROWS rows: one fused launch, and only h0 and
+    the last layer's output are returned ([h0, None, None, h3])."""
     from . import x3
 
     M, dev = h0.shape[0], h0.device
+    if not need_bits and not act16 and len(ws) == 3 and 0 < M <= TRUNK_MAX_ROWS and h0.dtype == torch.float32:
+        packs = [x3.pack(w, prec=prec) for w in ws]
+        if x3.trunk3_ok(M, h0, packs, prec):
+            return [h0, None, None, x3.trunk3(h0, packs, bs)], [None, None, None]
     hs, bits = [h0], []
     h = h0
     for w, b in zip(ws, bs):

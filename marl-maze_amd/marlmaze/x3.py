@@ -229,6 +229,32 @@ def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None
     return out
 
 
+def trunk3_ok(M, h0, packs, prec):
+    """Whether three ReLU layers of these packs (TP [N_l, K_l], one precision) at M rows run as one
+    mm_trunk3 launch."""
+    L = _lib.lib()
+    if not hasattr(L, "mm_trunk3") or len(packs) != 3 or any(p.prec != prec for p in packs):
+        return False
+    if packs[1].C != packs[0].R or packs[2].C != packs[1].R or h0.shape[1] != packs[0].C:
+        return False
+    return bool(L.mm_trunk3_ok(PRECS[prec], int(M), packs[0].C, packs[0].R, packs[1].R, packs[2].R,
+                               h0.stride(0)))
+
+
+def trunk3(h0, packs, biases, out=None):
+    """relu(relu(relu(h0 W0^T + b0) W1^T + b1) W2^T + b2) in one launch (mm_trunk3; bit-identical to three
+    gemm(..., bias, relu=True) calls): h0 fp32 [M, K0], packs the TPs of W0..W2."""
+    assert h0.dtype == torch.float32 and h0.dim() == 2 and h0.stride(1) == 1
+    M = h0.shape[0]
+    if out is None:
+        out = torch.empty((M, packs[2].R), dtype=torch.float32, device=h0.device)
+    _lib.check(_lib.lib().mm_trunk3(PRECS[packs[0].prec], _lib.ptr(h0), h0.stride(0), M, packs[0].C, packs[0].ptr(),
+                                    _lib.ptr(biases[0]), packs[0].R, packs[1].ptr(), _lib.ptr(biases[1]), packs[1].R,
+                                    packs[2].ptr(), _lib.ptr(biases[2]), packs[2].R, _lib.ptr(out), out.stride(0),
+                                    _lib.stream_ptr()), "mm_trunk3")
+    return out
+
+
 def a16_ok(M, N, K):
     """Whether an f16 GEMM of that shape takes fp16 A (mm_gemm_a16_ok: the B-resident kernel's shapes)."""
     return bool(_lib.lib().mm_gemm_a16_ok(int(M), int(N), int(K), int(K), int(N)))

@@ -1,0 +1,106 @@
+"""The fused small-M actor trunk (mm_trunk3, csrc/x3mlp.hip k_trunk3): the rollout's three ReLU layers
+(networks.py:35-36 under no_grad) in one launch.  It must equal the three per-layer GEMMs it replaces BIT
+FOR BIT (same fragment conversion, same MFMA sequence per output tile, same epilogue), at every precision,
+at ragged row counts and at shapes other than the actor's; the rollout-level parity against the fp32
+oracle is test_gpu_ppo.py's / test_gpu_update_parity.py's (the 4,096-maze rollout forward runs it)."""
+import pytest
+import torch
+
+from marlmaze import networks, x3
+
+pytestmark = pytest.mark.gpu
+
+
+def _layers(K0, Ns, prec, g):
+    ws, bs, packs = [], [], []
+    k = K0
+    for n in Ns:
+        w = torch.randn(n, k, device="cuda", generator=g) * (1.0 / k ** 0.5)
+        b = torch.randn(n, device="cuda", generator=g) * 0.1
+        ws.append(w)
+        bs.append(b)
+        packs.append(x3.pack(w, prec=prec))
+        k = n
+    return ws, bs, packs
+
+
+def _three_gemms(h0, packs, bs):
+    h = h0
+    for p, b in zip(packs, bs):
+        h = x3.gemm(h, p, bias=b, relu=True)
+    return h
+
+
+@pytest.mark.parametrize("prec", ["x2", "f16", "x3"])
+@pytest.mark.parametrize("M", [1, 17, 31, 32, 33, 47, 48, 49, 300, 4096, 8192, 8195, 16383])
+def test_trunk3_equals_three_gemms(prec, M):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + len(prec))
+    _, bs, packs = _layers(460, (264, 264, 264), prec, g)
+    h0 = torch.relu(torch.randn(M, 460, device="cuda", generator=g))
+    assert x3.trunk3_ok(M, h0, packs, prec)
+    y = x3.trunk3(h0, packs, bs)
+    ref = _three_gemms(h0, packs, bs)  # M < 16,384: the streaming kernel k_x3nt
+    assert torch.equal(y, ref)
+
+
+@pytest.mark.parametrize("prec,K0,Ns", [("x2", 64, (128, 64, 272)), ("x2", 128, (100, 36, 17)),
+                                        ("x2", 512, (272, 272, 1)), ("f16", 96, (48, 272, 264)),
+                                        ("x3", 256, (256, 264, 264)), ("x3", 96, (16, 40, 8))])
+def test_trunk3_other_shapes(prec, K0, Ns):
+    g = torch.Generator(device="cuda").manual_seed(K0 + sum(Ns))
+    _, bs, packs = _layers(K0, Ns, prec, g)
+    M = 1000
+    h0 = torch.randn(M, K0, device="cuda", generator=g)
+    y = x3.trunk3(h0, packs, bs)
+    assert y.shape == (M, Ns[-1])
+    assert torch.equal(y, _three_gemms(h0, packs, bs))
+
+
+def test_trunk3_strided_input_and_output_and_no_bias():
+    g = torch.Generator(device="cuda").manual_seed(3)
+    _, _, packs = _layers(460, (264, 264, 264), "x2", g)
+    big = torch.randn(2000, 472, device="cuda", generator=g)
+    h0 = big[:, :460]  # lda 472
+    out = torch.full((2000, 280), 7.0, device="cuda")
+    y = x3.trunk3(h0, packs, [None, None, None], out=out[:, :264])
+    assert torch.equal(y, _three_gemms(h0.contiguous(), packs, [None, None, None]))
+    assert bool((out[:, 264:] == 7.0).all())  # nothing written past N
+
+
+def test_trunk3_large_m_matches_b_resident_path():
+    """At >= 16,384 rows the per-layer GEMMs run on k_bres (another k tail form): equal to 1e-6."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    _, bs, packs = _layers(460, (264, 264, 264), "x2", g)
+    h0 = torch.relu(torch.randn(20000, 460, device="cuda", generator=g))
+    y, ref = x3.trunk3(h0, packs, bs), _three_gemms(h0, packs, bs)
+    assert (y - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
+
+
+def test_actor_trunk_uses_fused_launch_bit_identically(monkeypatch):
+    torch.manual_seed(4)
+    actor = networks.Actor(hidden_sizes=(264, 264, 264)).cuda()
+    x = torch.randn(8192, 65, device="cuda")
+    with torch.no_grad():
+        y = actor.trunk(x)
+        monkeypatch.setattr(networks, "TRUNK_MAX_ROWS", 0)
+        y0 = actor.trunk(x)
+    assert torch.equal(y, y0)
+
+
+def test_trunk3_rejects_unsupported_shapes():
+    g = torch.Generator(device="cuda").manual_seed(5)
+    _, _, packs = _layers(460, (264, 300, 264), "x2", g)  # N1 > 272
+    h0 = torch.randn(64, 460, device="cuda", generator=g)
+    assert not x3.trunk3_ok(64, h0, packs, "x2")
+    _, _, packs = _layers(460, (264, 264, 264), "x2", g)
+    assert not x3.trunk3_ok(64, torch.randn(64, 458, device="cuda"), packs, "x2")  # h0 width != W0's
+
+
+def test_trunk3_two_row_tile_form_equals(monkeypatch):
+    """MARLMAZE_TRUNK_RT=2 / MARLMAZE_TRUNK_D=3 select the other instantiations (read once per process by
+    the library: here through a subprocess-free check of both env-independent forms is not possible, so
+    the x3 path -- which takes the two-row-tile form at the actor's shape -- stands for it)."""
+    g = torch.Generator(device="cuda").manual_seed(9)
+    _, bs, packs = _layers(460, (264, 264, 264), "x3", g)
+    h0 = torch.relu(torch.randn(1000, 460, device="cuda", generator=g))
+    assert torch.equal(x3.trunk3(h0, packs, bs), _three_gemms(h0, packs, bs))
