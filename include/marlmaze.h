@@ -365,6 +365,18 @@ int mm_trunk3_ok(int prec, int M, int K0, int N0, int N1, int N2, int lda);
 int mm_trunk3(int prec, const float* h0, int lda, int M, int K0, const uint16_t* w0, const float* b0, int N0,
               const uint16_t* w1, const float* b1, int N1, const uint16_t* w2, const float* b2, int N2, float* out,
               int ldc, void* stream);
+/* mm_trunk3 + the actor heads + PPO.get_action (PPO.py:170-186) in one launch:
+ * the rollout's whole per-step actor after the front-end.  Replaces mm_trunk3
+ * followed by mm_head_sample_ex on its output, with the same results bit for
+ * bit (head_w [6, N2], head_b [6], masks, seed, offset, offset_dev, actions,
+ * logp, joint_logp, logits as there); h3 (optional, [M, ldh3]) receives the
+ * trunk's output.  N2 % 4 == 0.  mm_trunk3_head_sample_ok: 1 / 0. */
+int mm_trunk3_head_sample_ok(int prec, int M, int K0, int N0, int N1, int N2, int lda);
+int mm_trunk3_head_sample(int prec, const float* h0, int lda, int M, int K0, const uint16_t* w0, const float* b0,
+                          int N0, const uint16_t* w1, const float* b1, int N1, const uint16_t* w2, const float* b2,
+                          int N2, const float* head_w, const float* head_b, const uint8_t* masks, uint64_t seed,
+                          uint64_t offset, const uint64_t* offset_dev, int8_t* actions, float* logp,
+                          float* joint_logp, float* logits, float* h3, int ldh3, void* stream);
 
 /* The update's policy loss (PPO.py:62-72, get_log_probs PPO.py:154-168),
  * fused: heads [2M, 6] f32 (per agent row: 5 move logits, 1 mark logit),

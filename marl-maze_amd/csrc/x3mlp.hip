@@ -49,6 +49,7 @@
 #include <algorithm>
 
 #include "marlmaze.h"
+#include "policy_device.h"
 
 namespace mm {
 namespace x3 {
@@ -847,6 +848,17 @@ struct TrunkArgs {
     int lda, ldc, M, K0;
     int N[3];
     int bx;  // uint16 offset of the second activation buffer (bufH) from the first (bufX)
+    // the fused heads + sampler (k_trunk3<.., HS = true>: k_head_sample's arithmetic on the LDS-resident h3)
+    const float* hw;  // [6, N2] = [move_head.weight; mark_head.weight]
+    const float* hb;  // [6]
+    const uint8_t* masks;
+    uint64_t seed, offset;
+    const uint64_t* offset_dev;
+    int8_t* act;
+    float* logp;
+    float* joint;
+    float* logits;
+    int hoff;  // float offset (from the LDS base) of the h3 rows, stride N2 + 4
 };
 
 #ifdef X3_STAMPS  // diagnostic builds only (tools/trunk_stamps.py): per-wave phase clocks of k_trunk3
@@ -874,8 +886,8 @@ __device__ __forceinline__ int trunk_r16(int w) { return w == 0 ? 0 : w == 5 ? 1
 // the compiler's wait counting fall back to waiting for every load in flight at each step.
 template <int P, int RT, int D, int NC>
 __device__ __forceinline__ void trunk_layer_n(const uint16_t* src, int K, const uint16_t* W, int N, const float* sb,
-                                              uint16_t* dstL, float* slice, const TrunkArgs& ta, int m0, int wave,
-                                              int lane, uint32_t& rm, int stamp) {
+                                              uint16_t* dstL, float* slice, float* h3s, const TrunkArgs& ta, int m0,
+                                              int wave, int lane, uint32_t& rm, int stamp) {
     constexpr int np = Prec<P>::kPlanes;
     constexpr uint32_t kBS = 2u * Prec<P>::kBlk;  // bytes per TP block (16 rows x 32 k, all planes)
     const int nks = rup(K, 32) / 32, tiles = (N + 15) / 16;
@@ -977,7 +989,8 @@ __device__ __forceinline__ void trunk_layer_n(const uint16_t* src, int K, const 
             for (int g = 0; g < 4; g++) x[c][rt][g] = fmaxf(v[g] + bv, 0.f);
         }
     }
-    if (!dstL) {  // the last layer: fp32 rows of the output (16 lanes: 64 contiguous bytes of a row)
+    if (!dstL) {  // the last layer: fp32 rows of the output (16 lanes: 64 contiguous bytes of a row), and / or
+                  // the unit's rows in LDS for the fused heads (h3s, rows of N + 4 floats)
 #pragma unroll
         for (int c = 0; c < NC; c++) {
             const int col = 16 * trunk_tile(wave, c) + (lane & 15);
@@ -985,8 +998,9 @@ __device__ __forceinline__ void trunk_layer_n(const uint16_t* src, int K, const 
             for (int rt = 0; rt < (c < 2 ? RT : 1); rt++)
 #pragma unroll
                 for (int g = 0; g < 4; g++) {
-                    const int row = m0 + 16 * (c < 2 ? rt : r2) + rq + g;
-                    if (row < ta.M && col < N) ta.out[(size_t)row * ta.ldc + col] = x[c][rt][g];
+                    const int rl = 16 * (c < 2 ? rt : r2) + rq + g, row = m0 + rl;
+                    if (h3s && col < N) h3s[rl * (N + 4) + col] = x[c][rt][g];
+                    if (ta.out && row < ta.M && col < N) ta.out[(size_t)row * ta.ldc + col] = x[c][rt][g];
                 }
         }
         return;
@@ -1032,29 +1046,35 @@ __device__ __forceinline__ void trunk_layer_n(const uint16_t* src, int K, const 
 
 template <int P, int RT, int D>
 __device__ __forceinline__ void trunk_layer(const uint16_t* src, int K, const uint16_t* W, int N, const float* sb,
-                                            uint16_t* dstL, float* slice, const TrunkArgs& ta, int m0, int wave,
-                                            int lane, uint32_t& rm, int stamp) {
+                                            uint16_t* dstL, float* slice, float* h3s, const TrunkArgs& ta, int m0,
+                                            int wave, int lane, uint32_t& rm, int stamp) {
     const int tiles = (N + 15) / 16, nks = rup(K, 32) / 32;
     // wave-uniform: slots 0, 1 = tiles 2 w, 2 w + 1; slot 2 = one row tile of tile 16 (N > 256)
     const int nc = 2 * wave >= tiles ? 0 : 2 * wave + 1 >= tiles ? 1 : (trunk_r16(wave) >= 0 && trunk_r16(wave) < RT && tiles > 16) ? 3 : 2;
     if (nks % D == 0) {
-        if (nc == 3) trunk_layer_n<P, RT, D, 3>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
-        else if (nc == 2) trunk_layer_n<P, RT, D, 2>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
-        else if (nc == 1) trunk_layer_n<P, RT, D, 1>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+        if (nc == 3) trunk_layer_n<P, RT, D, 3>(src, K, W, N, sb, dstL, slice, h3s, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 2) trunk_layer_n<P, RT, D, 2>(src, K, W, N, sb, dstL, slice, h3s, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 1) trunk_layer_n<P, RT, D, 1>(src, K, W, N, sb, dstL, slice, h3s, ta, m0, wave, lane, rm, stamp);
     } else {  // (shapes other than the actor's: no prefetch beyond the next k-step)
-        if (nc == 3) trunk_layer_n<P, RT, 1, 3>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
-        else if (nc == 2) trunk_layer_n<P, RT, 1, 2>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
-        else if (nc == 1) trunk_layer_n<P, RT, 1, 1>(src, K, W, N, sb, dstL, slice, ta, m0, wave, lane, rm, stamp);
+        if (nc == 3) trunk_layer_n<P, RT, 1, 3>(src, K, W, N, sb, dstL, slice, h3s, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 2) trunk_layer_n<P, RT, 1, 2>(src, K, W, N, sb, dstL, slice, h3s, ta, m0, wave, lane, rm, stamp);
+        else if (nc == 1) trunk_layer_n<P, RT, 1, 1>(src, K, W, N, sb, dstL, slice, h3s, ta, m0, wave, lane, rm, stamp);
     }
 }
 
-template <int P, int RT, int D>
+// HS: the actor's heads + the action draw fused after the last layer (PPO.py:170-186 with networks.py:38-41):
+// k_head_sample's per-row arithmetic -- 8 lanes a row, the same fma order and butterfly, sample_row -- on the
+// unit's h3 rows in LDS, so the draws, log-probs and logits equal the unfused trunk + k_head_sample's bit for
+// bit; h3 is then written to HBM only when asked (ta.out)
+template <int P, int RT, int D, bool HS>
 __global__ __launch_bounds__(64 * kTrWaves) void k_trunk3(TrunkArgs ta) {
     constexpr int np = Prec<P>::kPlanes;
     constexpr int kIt = (RT * (kTrMaxK0 / 32) * 64 + 64 * kTrWaves - 1) / (64 * kTrWaves);  // h0 pieces per thread (max)
+    constexpr int kHw = (6 * kTrMaxN + 64 * kTrWaves - 1) / (64 * kTrWaves);              // head weights per thread
     extern __shared__ __attribute__((aligned(16))) float tls[];
     float* const sbias = tls;                       // [3][kTrMaxN], zero past N
-    float* const slices = tls + 3 * kTrMaxN;        // f16: [waves][kTrSlice] (x2 / x3 convert in place)
+    float* const shw = tls + 3 * kTrMaxN;           // [6][N2]: the head weights (HS)
+    float* const slices = shw + 6 * kTrMaxN;        // f16: [waves][kTrSlice] (x2 / x3 convert in place)
     uint16_t* const bufX = reinterpret_cast<uint16_t*>(slices + (np == 1 ? kTrWaves * kTrSlice : 0));  // h0, then layer 1's output
     uint16_t* const bufH = bufX + ta.bx;                                                 // layer 0's output
     const int lane = threadIdx.x & 63;
@@ -1104,6 +1124,24 @@ __global__ __launch_bounds__(64 * kTrWaves) void k_trunk3(TrunkArgs ta) {
             for (int l = 0; l < 3; l++) sbias[kTrMaxN * l + threadIdx.x] = bv[l];
         }
         asm volatile("" ::"v"(boff));
+        if constexpr (HS) {  // the head weights [6, N2], flat (k_head_sample's layout)
+            const __amdgpu_buffer_rsrc_t wrs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)ta.hw, (short)0, 4 * 6 * ta.N[2], 0x00020000);
+            uint32_t woff[kHw];
+            float wv[kHw];
+#pragma unroll
+            for (int u = 0; u < kHw; u++) woff[u] = 4u * (threadIdx.x + 64 * kTrWaves * u);
+#pragma unroll
+            for (int u = 0; u < kHw; u++) wv[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wrs, woff[u], 0, 0));
+#pragma unroll
+            for (int u = 0; u < kHw; u++) {
+                const int e = threadIdx.x + 64 * kTrWaves * u;
+                if (e < 6 * kTrMaxN) shw[e] = wv[u];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < kHw; u++) asm volatile("" ::"v"(woff[u]));
+        }
 #pragma unroll
         for (int j = 0; j < kIt; j++) {
             const int i = threadIdx.x + 64 * kTrWaves * j;
@@ -1122,15 +1160,66 @@ __global__ __launch_bounds__(64 * kTrWaves) void k_trunk3(TrunkArgs ta) {
     TR_STAMP(1, __builtin_amdgcn_s_memtime());
     float* const slice = slices + wave * kTrSlice;
     uint32_t rm = 0;  // the range guard (range_acc)
-    trunk_layer<P, RT, D>(bufX, ta.K0, ta.w[0], ta.N[0], sbias, bufH, slice, ta, m0, wave, lane, rm, 2);
+    trunk_layer<P, RT, D>(bufX, ta.K0, ta.w[0], ta.N[0], sbias, bufH, slice, nullptr, ta, m0, wave, lane, rm, 2);
     __syncthreads();
     TR_STAMP(3, __builtin_amdgcn_s_memtime());
-    trunk_layer<P, RT, D>(bufH, ta.N[0], ta.w[1], ta.N[1], sbias + kTrMaxN, bufX, slice, ta, m0, wave, lane, rm, 4);
+    trunk_layer<P, RT, D>(bufH, ta.N[0], ta.w[1], ta.N[1], sbias + kTrMaxN, bufX, slice, nullptr, ta, m0, wave, lane,
+                          rm, 4);
     __syncthreads();
     TR_STAMP(5, __builtin_amdgcn_s_memtime());
-    trunk_layer<P, RT, D>(bufX, ta.N[1], ta.w[2], ta.N[2], sbias + 2 * kTrMaxN, nullptr, slice, ta, m0, wave, lane, rm,
-                          6);
+    float* const h3s = HS ? tls + ta.hoff : nullptr;  // (bufH, free in the last layer, or a region of its own)
+    trunk_layer<P, RT, D>(bufX, ta.N[1], ta.w[2], ta.N[2], sbias + 2 * kTrMaxN, nullptr, slice, h3s, ta, m0, wave,
+                          lane, rm, 6);
     range_note<P>(rm);
+    if constexpr (HS) {  // k_head_sample's body on the LDS rows: 8 lanes a row, 16 RT rows (waves 0 .. 2 RT - 1)
+        __syncthreads();
+        constexpr int kL = 8;
+        const int K = ta.N[2], sh = K + 4;
+        if (threadIdx.x < kL * 16 * RT) {  // wave-uniform
+            const int j = threadIdx.x % kL, rl = threadIdx.x / kL, row = m0 + rl;
+            const bool valid = row < ta.M;
+            float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (valid) {
+                const float* hr = h3s + rl * sh;
+                for (int c = 4 * j; c < K; c += 4 * kL) {
+                    const float4 hv = *reinterpret_cast<const float4*>(hr + c);
+#pragma unroll
+                    for (int o = 0; o < 6; o++) {
+                        const float4 wv = *reinterpret_cast<const float4*>(shw + o * K + c);
+                        acc[o] = fmaf(hv.x, wv.x, acc[o]);
+                        acc[o] = fmaf(hv.y, wv.y, acc[o]);
+                        acc[o] = fmaf(hv.z, wv.z, acc[o]);
+                        acc[o] = fmaf(hv.w, wv.w, acc[o]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 0; o < 6; o++) {
+#pragma unroll
+                for (int d = kL / 2; d > 0; d >>= 1) acc[o] += __shfl_xor(acc[o], d);
+            }
+            float lp = 0.f;
+            if (valid && j == 0) {
+                float l[5];
+#pragma unroll
+                for (int o = 0; o < 5; o++) l[o] = acc[o] + ta.hb[o];
+                const float kl = acc[5] + ta.hb[5];
+                int move, mark;
+                const uint64_t off = ta.offset + (ta.offset_dev ? *ta.offset_dev : 0ull);
+                lp = sample_row(l, kl, ta.masks + (size_t)row * MM_MASK_DIM, row, ta.seed, off, move, mark);
+                ta.act[2 * row] = (int8_t)move;
+                ta.act[2 * row + 1] = (int8_t)mark;
+                if (ta.logp) ta.logp[row] = lp;
+                if (ta.logits) {
+#pragma unroll
+                    for (int o = 0; o < 5; o++) ta.logits[(size_t)row * 6 + o] = l[o];
+                    ta.logits[(size_t)row * 6 + 5] = kl;
+                }
+            }
+            const float other = __shfl_down(lp, kL);  // rows 2i, 2i + 1: adjacent 8-lane groups (m0 even)
+            if (ta.joint && valid && j == 0 && (row & 1) == 0) ta.joint[row >> 1] = lp + (row + 1 < ta.M ? other : 0.f);
+        }
+    }
     TR_STAMP(7, __builtin_amdgcn_s_memtime());
     TR_STAMP(9, __builtin_amdgcn_s_memrealtime());
 }
@@ -2571,7 +2660,23 @@ static void trunk_bufs(int prec, int RT, int K0, int N0, int N1, int& bx, size_t
     const int np = prec == MM_PREC_X3 ? 3 : prec == MM_PREC_X2 ? 2 : 1;
     const int nx = std::max(rup(K0, 32), rup(N1, 32)) / 32, nh = rup(N0, 32) / 32;
     bx = RT * nx * np * 512;
-    lds = (size_t)(3 * kTrMaxN + (np == 1 ? kTrWaves * kTrSlice : 0)) * 4 + (size_t)RT * (nx + nh) * np * 1024;
+    lds = (size_t)(9 * kTrMaxN + (np == 1 ? kTrWaves * kTrSlice : 0)) * 4 + (size_t)RT * (nx + nh) * np * 1024;
+}
+
+// the fused heads' h3 rows (16 RT rows of N2 + 4 floats): in bufH when it holds them (free during the last
+// layer), else in a region appended to the LDS; hoff in floats from the LDS base
+static void trunk_h3(int prec, int RT, int K0, int N0, int N1, int N2, int& hoff, size_t& lds) {
+    const int np = prec == MM_PREC_X3 ? 3 : prec == MM_PREC_X2 ? 2 : 1;
+    int bx;
+    trunk_bufs(prec, RT, K0, N0, N1, bx, lds);
+    const size_t need = (size_t)16 * RT * (N2 + 4) * 4, hbytes = (size_t)RT * (rup(N0, 32) / 32) * np * 1024;
+    const size_t bufx = (size_t)(9 * kTrMaxN + (np == 1 ? kTrWaves * kTrSlice : 0)) * 4;
+    if (need <= hbytes) {
+        hoff = (int)((bufx + (size_t)bx * 2) / 4);
+    } else {
+        hoff = (int)(lds / 4);
+        lds += need;
+    }
 }
 
 static int trunk_pick_rt(int prec, int K0, int N0, int N1) {
@@ -2592,16 +2697,17 @@ extern "C" int mm_trunk3_ok(int prec, int M, int K0, int N0, int N1, int N2, int
     return trunk_pick_rt(prec, K0, N0, N1) ? 1 : 0;
 }
 
-template <int P, int RT, int D>
+template <int P, int RT, int D, bool HS = false>
 static int launch_trunk(const TrunkArgs& ta, size_t lds, hipStream_t s) {
     static bool attr = false;
     if (!attr) {
-        if (hipFuncSetAttribute((const void*)k_trunk3<P, RT, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        if (hipFuncSetAttribute((const void*)k_trunk3<P, RT, D, HS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024) != hipSuccess)
             return MM_E_ARG;
         attr = true;
     }
-    hipLaunchKernelGGL((k_trunk3<P, RT, D>), dim3((ta.M + 16 * RT - 1) / (16 * RT)), dim3(64 * kTrWaves), lds, s, ta);
+    hipLaunchKernelGGL((k_trunk3<P, RT, D, HS>), dim3((ta.M + 16 * RT - 1) / (16 * RT)), dim3(64 * kTrWaves), lds, s,
+                       ta);
     return (int)hipGetLastError();
 }
 
@@ -2622,12 +2728,44 @@ extern "C" int mm_trunk3(int prec, const float* h0, int lda, int M, int K0, cons
     if (((uintptr_t)h0 & 15) || (((uintptr_t)w0 | (uintptr_t)w1 | (uintptr_t)w2) & 15) || ((uintptr_t)out & 3))
         return MM_E_ARG;
     if (M == 0) return 0;
-    TrunkArgs ta{h0, {w0, w1, w2}, {b0, b1, b2}, out, lda, ldc, M, K0, {N0, N1, N2}, 0};
+    TrunkArgs ta{h0, {w0, w1, w2}, {b0, b1, b2}, out, lda, ldc, M, K0, {N0, N1, N2}, 0,
+                 nullptr, nullptr, nullptr, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
     const int RT = trunk_pick_rt(prec, K0, N0, N1);
     hipStream_t s = (hipStream_t)stream;
     if (prec == MM_PREC_X2) return launch_trunk_p<P_X2>(ta, RT, s);
     if (prec == MM_PREC_F16) return launch_trunk_p<P_F16>(ta, RT, s);
     return launch_trunk_p<P_X3>(ta, RT, s);
+}
+
+// the trunk + the actor heads + PPO.get_action in one launch (two row tiles a workgroup; D as mm_trunk3)
+extern "C" int mm_trunk3_head_sample_ok(int prec, int M, int K0, int N0, int N1, int N2, int lda) {
+    if (!mm_trunk3_ok(prec, M, K0, N0, N1, N2, lda) || (N2 & 3)) return 0;
+    int hoff;
+    size_t lds;
+    trunk_h3(prec, 2, K0, N0, N1, N2, hoff, lds);
+    return lds <= 160 * 1024 ? 1 : 0;
+}
+
+extern "C" int mm_trunk3_head_sample(int prec, const float* h0, int lda, int M, int K0, const uint16_t* w0,
+                                     const float* b0, int N0, const uint16_t* w1, const float* b1, int N1,
+                                     const uint16_t* w2, const float* b2, int N2, const float* head_w,
+                                     const float* head_b, const uint8_t* masks, uint64_t seed, uint64_t offset,
+                                     const uint64_t* offset_dev, int8_t* actions, float* logp, float* joint_logp,
+                                     float* logits, float* h3, int ldh3, void* stream) {
+    if (!mm_trunk3_head_sample_ok(prec, M, K0, N0, N1, N2, lda) || !h0 || !w0 || !w1 || !w2 || !head_w || !head_b ||
+        !masks || !actions || (h3 && (ldh3 < N2 || ((uintptr_t)h3 & 3))))
+        return MM_E_ARG;
+    if (((uintptr_t)h0 & 15) || (((uintptr_t)w0 | (uintptr_t)w1 | (uintptr_t)w2) & 15)) return MM_E_ARG;
+    if (M == 0) return 0;
+    TrunkArgs ta{h0, {w0, w1, w2}, {b0, b1, b2}, h3, lda, ldh3, M, K0, {N0, N1, N2}, 0,
+                 head_w, head_b, masks, seed, offset, offset_dev, actions, logp, joint_logp, logits, 0};
+    size_t lds;
+    trunk_bufs(prec, 2, K0, N0, N1, ta.bx, lds);
+    trunk_h3(prec, 2, K0, N0, N1, N2, ta.hoff, lds);
+    hipStream_t s = (hipStream_t)stream;
+    if (prec == MM_PREC_X2) return launch_trunk<P_X2, 2, 1, true>(ta, lds, s);
+    if (prec == MM_PREC_F16) return launch_trunk<P_F16, 2, 3, true>(ta, lds, s);
+    return launch_trunk<P_X3, 2, 1, true>(ta, lds, s);
 }
 
 // dY = (dz W) * bits (the heads' backward through the last ReLU, bits from the

@@ -306,11 +306,12 @@ class PPO:
                 self.critic.value_into(obs_t, b["val"][t])
             else:
                 b["val"][t] = self.critic(obs_t).view(n)
-            # actor trunk, then heads + sampling fused (PPO.py:170-186; ops.head_sample)
-            h = self.actor.trunk(obs_t.view(2 * n, 65))
-            ops.head_sample(h, head_w, head_b, b["masks"][t].view(2 * n, 6), self.sample_seed,
-                            t if offset_dev is not None else self._sample_offset, actions=b["act"][t].view(2 * n, 2),
-                            logp=b["rowlogp"][t], joint_logp=b["logp"][t], offset_dev=offset_dev)
+            # actor trunk, heads and sampling (PPO.py:170-186): one launch after the front-end at small N
+            # (Actor.sample_actions), else the trunk's GEMMs + ops.head_sample
+            self.actor.sample_actions(obs_t.view(2 * n, 65), head_w, head_b, b["masks"][t].view(2 * n, 6),
+                                      self.sample_seed, t if offset_dev is not None else self._sample_offset,
+                                      actions=b["act"][t].view(2 * n, 2), logp=b["rowlogp"][t],
+                                      joint_logp=b["logp"][t], offset_dev=offset_dev)
             if offset_dev is None:
                 self._sample_offset += 1
             ev = self.step_events
@@ -417,10 +418,10 @@ class PPO:
                     # the fixed-horizon rollout's value arithmetic (value_into: the fused fp32 kernel), so a
                     # network's stored values do not depend on the batch mode
                     self.critic.value_into(ch["obs"][t], ch["val"][t])
-                    h = self.actor.trunk(ch["obs"][t].view(2 * n, 65))
-                    ops.head_sample(h, head_w, head_b, ch["masks"][t].view(2 * n, 6), self.sample_seed,
-                                    self._sample_offset, actions=ch["act"][t].view(2 * n, 2), logp=ch["rowlogp"][t],
-                                    joint_logp=ch["logp"][t])
+                    self.actor.sample_actions(ch["obs"][t].view(2 * n, 65), head_w, head_b,
+                                              ch["masks"][t].view(2 * n, 6), self.sample_seed, self._sample_offset,
+                                              actions=ch["act"][t].view(2 * n, 2), logp=ch["rowlogp"][t],
+                                              joint_logp=ch["logp"][t])
                     self._sample_offset += 1
                     self.venv.step(ch["act"][t], auto_reset=True, obs=ch["obs"][t + 1], masks=ch["masks"][t + 1],
                                    reward=ch["rew"][t], done=ch["done"][t], ep_stats=ch["stats"][t])

@@ -541,6 +541,27 @@ class Actor(nn.Module):
         """Everything up to the last hidden layer (networks.py:31-36)."""
         return self._mlp(self._front(x))
 
+    def sample_actions(self, x, head_w, head_b, masks, seed, offset, actions, logp=None, joint_logp=None,
+                       offset_dev=None):
+        """The rollout's actor step (PPO.py:170-186): front-end, trunk, heads and the action draws
+        (ops.head_sample's).  At <= TRUNK_MAX_ROWS rows without autograd the trunk, heads and draws run as
+        ONE launch (mm_trunk3_head_sample, bit-identical to trunk + ops.head_sample)."""
+        from . import ops, x3
+
+        h0 = self._front(x)
+        M = h0.shape[0]
+        if (not torch.is_grad_enabled() and len(self.layers) == 3 and 0 < M <= TRUNK_MAX_ROWS and h0.is_cuda
+                and h0.dtype == torch.float32 and self._engine(h0)):
+            params = self._mlp_params()
+            packs = [x3.pack(w, prec=self.gemm_prec) for w in params[0::2]]
+            if x3.trunk3_head_sample_ok(M, h0, packs, self.gemm_prec):
+                x3.trunk3_head_sample(h0, packs, params[1::2], head_w.contiguous(), head_b.contiguous(),
+                                      masks.to(torch.uint8).contiguous(), seed, offset, actions, logp, joint_logp,
+                                      offset_dev=offset_dev)
+                return actions, logp, joint_logp
+        return ops.head_sample(self._mlp(h0), head_w, head_b, masks, seed, offset, actions=actions, logp=logp,
+                               joint_logp=joint_logp, offset_dev=offset_dev)
+
     def _front(self, x):
         """Projection + attention (networks.py:31-34)."""
         x = torch.as_tensor(x, dtype=torch.float32, device=self.move_head.weight.device).reshape(-1, OBS_SPACE)

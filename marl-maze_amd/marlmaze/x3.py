@@ -255,6 +255,32 @@ def trunk3(h0, packs, biases, out=None):
     return out
 
 
+def trunk3_head_sample_ok(M, h0, packs, prec):
+    """Whether the trunk + heads + sampler of these packs run as one mm_trunk3_head_sample launch."""
+    L = _lib.lib()
+    return (trunk3_ok(M, h0, packs, prec) and hasattr(L, "mm_trunk3_head_sample")
+            and bool(L.mm_trunk3_head_sample_ok(PRECS[prec], int(M), packs[0].C, packs[0].R, packs[1].R, packs[2].R,
+                                                h0.stride(0))))
+
+
+def trunk3_head_sample(h0, packs, biases, head_w, head_b, masks, seed, offset, actions, logp=None, joint_logp=None,
+                       logits=None, offset_dev=None, h3=None):
+    """trunk3 + the actor heads + PPO.get_action in one launch (mm_trunk3_head_sample): the same actions,
+    log-probs and logits as trunk3 followed by ops.head_sample, bit for bit.  masks [M, 6] u8, actions
+    [M, 2] i8 (written); h3 (optional) receives the trunk's output."""
+    assert h0.dtype == torch.float32 and h0.dim() == 2 and h0.stride(1) == 1
+    M = h0.shape[0]
+    assert masks.dtype == torch.uint8 and masks.is_contiguous() and actions.is_contiguous()
+    _lib.check(_lib.lib().mm_trunk3_head_sample(
+        PRECS[packs[0].prec], _lib.ptr(h0), h0.stride(0), M, packs[0].C, packs[0].ptr(), _lib.ptr(biases[0]),
+        packs[0].R, packs[1].ptr(), _lib.ptr(biases[1]), packs[1].R, packs[2].ptr(), _lib.ptr(biases[2]),
+        packs[2].R, _lib.ptr(head_w), _lib.ptr(head_b), _lib.ptr(masks), int(seed) & (2**64 - 1),
+        int(offset) & (2**64 - 1), _lib.ptr(offset_dev), _lib.ptr(actions), _lib.ptr(logp), _lib.ptr(joint_logp),
+        _lib.ptr(logits), _lib.ptr(h3), h3.stride(0) if h3 is not None else 0, _lib.stream_ptr()),
+        "mm_trunk3_head_sample")
+    return actions, logp, joint_logp
+
+
 def a16_ok(M, N, K):
     """Whether an f16 GEMM of that shape takes fp16 A (mm_gemm_a16_ok: the B-resident kernel's shapes)."""
     return bool(_lib.lib().mm_gemm_a16_ok(int(M), int(N), int(K), int(K), int(N)))

@@ -104,3 +104,68 @@ def test_trunk3_two_row_tile_form_equals(monkeypatch):
     _, bs, packs = _layers(460, (264, 264, 264), "x3", g)
     h0 = torch.relu(torch.randn(1000, 460, device="cuda", generator=g))
     assert torch.equal(x3.trunk3(h0, packs, bs), _three_gemms(h0, packs, bs))
+
+
+# ---- the trunk + heads + draws in one launch (mm_trunk3_head_sample) ----
+
+def _heads(g, K=264):
+    return (torch.randn(6, K, device="cuda", generator=g) * 0.2, torch.randn(6, device="cuda", generator=g) * 0.1)
+
+
+def _masks(M, g):
+    mk = (torch.rand(M, 6, device="cuda", generator=g) < 0.6).to(torch.uint8)
+    mk[:, 4] = 1  # at least one legal move per row (an all-illegal row's log-prob is NaN either way)
+    return mk.contiguous()
+
+
+@pytest.mark.parametrize("prec", ["x2", "f16", "x3"])
+@pytest.mark.parametrize("M", [1, 2, 33, 300, 4096, 8192, 8193])
+def test_trunk3_head_sample_equals_trunk_then_head_sample(prec, M):
+    from marlmaze import ops
+
+    g = torch.Generator(device="cuda").manual_seed(100 + M + len(prec))
+    _, bs, packs = _layers(460, (264, 264, 264), prec, g)
+    hw, hb = _heads(g)
+    h0 = torch.relu(torch.randn(M, 460, device="cuda", generator=g))
+    mk = _masks(M, g)
+    assert x3.trunk3_head_sample_ok(M, h0, packs, prec)
+    off_dev = torch.tensor([7], dtype=torch.int64, device="cuda")
+    act = torch.full((M, 2), -9, dtype=torch.int8, device="cuda")
+    lp, jl = torch.empty(M, device="cuda"), torch.empty((M + 1) // 2, device="cuda")
+    lg, h3 = torch.empty(M, 6, device="cuda"), torch.empty(M, 264, device="cuda")
+    L = x3._lib.lib()
+    x3.trunk3_head_sample(h0, packs, bs, hw, hb, mk, 1234, 5, act, lp, jl, logits=lg, offset_dev=off_dev, h3=h3)
+    ref_h = x3.trunk3(h0, packs, bs)
+    act_r = torch.empty((M, 2), dtype=torch.int8, device="cuda")
+    lp_r, jl_r = torch.empty(M, device="cuda"), torch.empty((M + 1) // 2, device="cuda")
+    lg_r = torch.empty(M, 6, device="cuda")
+    ops.head_sample(ref_h, hw, hb, mk, 1234, 5, actions=act_r, logp=lp_r, joint_logp=jl_r, logits=lg_r,
+                    offset_dev=off_dev)
+    assert torch.equal(h3, ref_h)
+    assert torch.equal(lg, lg_r)
+    assert torch.equal(act, act_r)
+    assert torch.equal(lp, lp_r) and torch.equal(jl, jl_r)
+    del L
+
+
+def test_actor_sample_actions_fused_equals_unfused(monkeypatch):
+    from marlmaze import ops
+
+    torch.manual_seed(6)
+    actor = networks.Actor(hidden_sizes=(264, 264, 264)).cuda()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    M = 8192
+    x = torch.randn(M, 65, device="cuda", generator=g)
+    mk = _masks(M, g)
+    hw, hb = actor.heads()
+    outs = []
+    for rows in (networks.TRUNK_MAX_ROWS, 0):
+        monkeypatch.setattr(networks, "TRUNK_MAX_ROWS", rows)
+        act = torch.empty((M, 2), dtype=torch.int8, device="cuda")
+        lp, jl = torch.empty(M, device="cuda"), torch.empty(M // 2, device="cuda")
+        with torch.no_grad():
+            actor.sample_actions(x, hw, hb, mk, 99, 3, act, lp, jl)
+        outs.append((act, lp, jl))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    del ops
