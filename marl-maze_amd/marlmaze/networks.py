@@ -241,20 +241,28 @@ def _act16(prec, M, widths, next_ks):
 
 
 # three ReLU layers without bits (the rollout's trunk) up to this many rows run as ONE launch (mm_trunk3:
-# bit-identical to the per-layer GEMMs, which sit at their launch floor there); 0 switches it off
-TRUNK_MAX_ROWS = int(os.environ.get("MARLMAZE_TRUNK_MAX_ROWS", "16384"))
+# bit-identical to the per-layer GEMMs below 16,384 rows, where those sit at their launch floor).  Per
+# precision, from tools/bench_trunk.py (profiles/r05_bench_trunk_*.jsonl; fused vs three GEMMs, HIP graphs):
+# x2 8,192 rows 21.8 vs 42.0 us, 49,152 124 vs 133 us; f16 65,536 81 vs 123 us, 131,072 162 vs 259 us.
+# MARLMAZE_TRUNK_MAX_ROWS overrides it for every precision (0: off).
+_TRUNK_MAX_ROWS_DEFAULT = {"x2": 49152, "x3": 16384, "f16": 131072}
+TRUNK_MAX_ROWS = int(os.environ["MARLMAZE_TRUNK_MAX_ROWS"]) if "MARLMAZE_TRUNK_MAX_ROWS" in os.environ else None
+
+
+def _trunk_max_rows(prec):
+    return TRUNK_MAX_ROWS if TRUNK_MAX_ROWS is not None else _TRUNK_MAX_ROWS_DEFAULT.get(prec, 0)
 
 
 def _mlp_fwd(h0, ws, bs, prec, need_bits, act16=False):
     """The ReLU layers on the engine; returns the activations [h0, h1, ...] and
     the forward GEMMs' ReLU bit masks (None without need_bits).  act16: the
     layers' outputs in fp16 (f16 with bits only, see F16_ACT).  Three layers
-    without bits at <= TRUNK_MAX_ROWS rows: one fused launch, and only h0 and
-    the last layer's output are returned ([h0, None, None, h3])."""
+    without bits at <= _trunk_max_rows(prec) rows: one fused launch, and only h0
+    and the last layer's output are returned ([h0, None, None, h3])."""
     from . import x3
 
     M, dev = h0.shape[0], h0.device
-    if not need_bits and not act16 and len(ws) == 3 and 0 < M <= TRUNK_MAX_ROWS and h0.dtype == torch.float32:
+    if not need_bits and not act16 and len(ws) == 3 and 0 < M <= _trunk_max_rows(prec) and h0.dtype == torch.float32:
         packs = [x3.pack(w, prec=prec) for w in ws]
         if x3.trunk3_ok(M, h0, packs, prec):
             return [h0, None, None, x3.trunk3(h0, packs, bs)], [None, None, None]
@@ -544,13 +552,13 @@ class Actor(nn.Module):
     def sample_actions(self, x, head_w, head_b, masks, seed, offset, actions, logp=None, joint_logp=None,
                        offset_dev=None):
         """The rollout's actor step (PPO.py:170-186): front-end, trunk, heads and the action draws
-        (ops.head_sample's).  At <= TRUNK_MAX_ROWS rows without autograd the trunk, heads and draws run as
+        (ops.head_sample's).  At <= _trunk_max_rows(prec) rows without autograd the trunk, heads and draws run as
         ONE launch (mm_trunk3_head_sample, bit-identical to trunk + ops.head_sample)."""
         from . import ops, x3
 
         h0 = self._front(x)
         M = h0.shape[0]
-        if (not torch.is_grad_enabled() and len(self.layers) == 3 and 0 < M <= TRUNK_MAX_ROWS and h0.is_cuda
+        if (not torch.is_grad_enabled() and len(self.layers) == 3 and 0 < M <= _trunk_max_rows(self.gemm_prec) and h0.is_cuda
                 and h0.dtype == torch.float32 and self._engine(h0)):
             params = self._mlp_params()
             packs = [x3.pack(w, prec=self.gemm_prec) for w in params[0::2]]

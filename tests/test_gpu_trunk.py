@@ -159,7 +159,7 @@ def test_actor_sample_actions_fused_equals_unfused(monkeypatch):
     mk = _masks(M, g)
     hw, hb = actor.heads()
     outs = []
-    for rows in (networks.TRUNK_MAX_ROWS, 0):
+    for rows in (None, 0):
         monkeypatch.setattr(networks, "TRUNK_MAX_ROWS", rows)
         act = torch.empty((M, 2), dtype=torch.int8, device="cuda")
         lp, jl = torch.empty(M, device="cuda"), torch.empty(M // 2, device="cuda")
