@@ -352,6 +352,10 @@ int mm_gemm_wgrad_partials_h(int prec, int flags, const float* dy, int lddy, flo
                              int M, int N, int K, float cscale, float* ws, void* stream);
 int mm_heads_fwd_h16(const void* h, int ldh, int K, const float* w, const float* b, int M, float* logits,
                      void* stream);
+/* mm_actor_front_fwd with h stored fp16 [B, 460] (round to nearest of the fp32
+ * values): the f16 networks' update, whose first GEMM (fp16 A at K = 460: the
+ * streaming kernel) and its weight gradient round h to fp16 anyway. */
+int mm_actor_front_fwd_h16(const float* ws, const float* x, int ldx, int B, int parity, void* h, void* stream);
 
 /* The actor trunk's three ReLU layers (networks.py:35-36) in one launch, for
  * the rollout's small row counts (BASELINE configs[1]: 8,192 rows per step,

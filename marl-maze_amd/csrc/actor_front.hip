@@ -350,8 +350,11 @@ __device__ __forceinline__ void stage_tables(const float* __restrict__ ws, float
     }
 }
 
+// H16: h stored as fp16 (the fp16 networks' update: their first trunk GEMM and its weight gradient round h to
+// fp16 anyway), rounded to nearest from the same fp32 values
+template <bool H16 = false>
 __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws, const float* __restrict__ x,
-                                                   int ldx, int B, int parity, float* __restrict__ h) {
+                                                   int ldx, int B, int parity, void* __restrict__ hv) {
     __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
     __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKq];
     __shared__ __attribute__((aligned(16))) float Vs[kFwdRows][kTok][kEmb];
@@ -407,11 +410,20 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
             for (int j = 0; j < kTok; j++) axpy4<kEmb>(out, s[j] * inv, Vs[g][j]);
             float t[kEmb];
             affine4t<kEmb>(ti + kQkv * (kPin + 1), ti + kQkv * (kPin + 1) + kEmb * kPin, xv, t);
-            float* o = h + (size_t)row * kRowF + i * kEmb;
+            if constexpr (H16) {
+                typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+                _Float16* o = static_cast<_Float16*>(hv) + (size_t)row * kRowF + i * kEmb;
 #pragma unroll
-            for (int c = 0; c < kEmb; c += 4)
-                *reinterpret_cast<float4*>(o + c) =
-                    make_float4(t[c] + out[c], t[c + 1] + out[c + 1], t[c + 2] + out[c + 2], t[c + 3] + out[c + 3]);
+                for (int c = 0; c < kEmb; c += 4)
+                    *reinterpret_cast<h4*>(o + c) = h4{(_Float16)(t[c] + out[c]), (_Float16)(t[c + 1] + out[c + 1]),
+                                                       (_Float16)(t[c + 2] + out[c + 2]), (_Float16)(t[c + 3] + out[c + 3])};
+            } else {
+                float* o = static_cast<float*>(hv) + (size_t)row * kRowF + i * kEmb;
+#pragma unroll
+                for (int c = 0; c < kEmb; c += 4)
+                    *reinterpret_cast<float4*>(o + c) =
+                        make_float4(t[c] + out[c], t[c + 1] + out[c + 1], t[c + 2] + out[c + 2], t[c + 3] + out[c + 3]);
+            }
         }
     }
 }
@@ -1469,8 +1481,19 @@ extern "C" int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, i
     } else {
         const int groups = (B + kFwdRows - 1) / kFwdRows;
         const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();  // three workgroups per CU
-        hipLaunchKernelGGL(k_front_fwd, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
+        hipLaunchKernelGGL(k_front_fwd<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity,
+                           (void*)h);
     }
+    return (int)hipGetLastError();
+}
+
+extern "C" int mm_actor_front_fwd_h16(const float* ws, const float* x, int ldx, int B, int parity, void* h,
+                                      void* stream) {
+    if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM || ((uintptr_t)h & 7)) return MM_E_ARG;
+    if (B == 0) return 0;
+    const int groups = (B + kFwdRows - 1) / kFwdRows;
+    const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();
+    hipLaunchKernelGGL(k_front_fwd<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
     return (int)hipGetLastError();
 }
 

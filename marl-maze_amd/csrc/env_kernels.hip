@@ -844,7 +844,7 @@ inline int check_env(const mm_env_t* env) {
 
 using namespace mm;
 
-extern "C" int mm_version(void) { return 306; }
+extern "C" int mm_version(void) { return 307; }
 
 extern "C" int mm_env_desc_size(void) { return (int)sizeof(mm_env_t); }
 

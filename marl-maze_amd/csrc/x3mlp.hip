@@ -462,6 +462,34 @@ struct ASrcF32V {
 typedef ASrcF32V<4> ASrcF32;
 typedef ASrcF32V<2> ASrcF32U;
 
+// fp16 row-major [M, lda] (P_F16 at scale 1: the f16 networks' stored front-end output h, K = 460, which the
+// B-resident kernel does not take): the lane's two 8-byte runs of 4 halves ARE its fragment, no conversion
+struct ASrcF16V {
+    typedef u32x2v Raw[2];
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t roff;  // this lane's row (clamped inside the matrix), column 4 (l >> 4), bytes
+    int K, kq;
+    __device__ void init(const unsigned short* base, int rt, int, int M, int lda, int K_, float) {
+        const int lane = threadIdx.x & 63;
+        const int r = min(16 * rt + (lane & 15), M - 1);  // rows past M: computed, never stored
+        K = K_;
+        kq = 4 * (lane >> 4);
+        rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((size_t)M * lda * 2), 0x00020000);
+        roff = 2u * ((uint32_t)r * (uint32_t)lda + (uint32_t)kq);
+    }
+    __device__ __forceinline__ void load(int ks, Raw& r, int) const {  // columns past K: zeros (out of range)
+        const int k = 32 * ks + kq;
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+            r[h] = __builtin_amdgcn_raw_buffer_load_b64(rs, k + 16 * h < K ? roff + 2u * (32 * ks + 16 * h) : kBufOOB, 0, 0);
+    }
+    template <int P>
+    __device__ __forceinline__ void frag(const Raw& r, bf16x8 (&a)[3]) const {
+        static_assert(P == P_F16, "fp16 A: P_F16");
+        a[0] = __builtin_bit_cast(bf16x8, make_uint4(r[0].x, r[0].y, r[1].x, r[1].y));
+    }
+};
+
 // One k-step on stage buffer `cur`: split this step's A (raw -> fragments),
 // prefetch the next step's raw A (registers) and B pieces (the other buffer;
 // the DMA issues spread over the column loop), the 6 x NT MFMAs, one barrier.
@@ -2592,8 +2620,14 @@ static int gemm_nt_f32a(int prec, const float* a, int lda, float ascale, const u
     hipStream_t s = (hipStream_t)stream;
     BresPlan pl;
     int cfg = C_NARROW;
-    if (a16 || (c16 && mbits_in)) {  // fp16 A, or fp16 input gradients: the B-resident kernel only
-        if (!bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) return MM_E_ARG;
+    if (a16 || (c16 && mbits_in)) {  // fp16 A, or fp16 input gradients: the B-resident kernel, or for fp16 A
+                                      // where it does not fit (K = 460) the streaming kernel with ASrcF16V
+        if (!bres_plan(prec, M, N, K, lda, ldc, mbits_in || mbits_out, pl, cfg)) {
+            if (a16 && !(c16 && mbits_in))
+                return dispatch_nt<P_F16, ASrcF16V>(reinterpret_cast<const unsigned short*>(a), lda, 1.f, b_tp, M, N,
+                                                    K, ep, s);
+            return MM_E_ARG;
+        }
         return a16 ? dispatch_bres<P_F16, 16>(a, lda, 1.f, b_tp, M, N, K, pl, cfg, ep, s)
                    : (v4 ? dispatch_bres<P_F16, 4>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s)
                          : dispatch_bres<P_F16, 2>(a, lda, ascale, b_tp, M, N, K, pl, cfg, ep, s));

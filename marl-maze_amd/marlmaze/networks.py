@@ -229,6 +229,8 @@ def _wgrad(dy, x, prec, out=None):
 # fp32 FMAs over fp16 values), so the arithmetic is that of fp32 storage at half the bytes.
 # MARLMAZE_F16_ACT=0 keeps them fp32 (A/B runs).
 F16_ACT = os.environ.get("MARLMAZE_F16_ACT", "1") != "0"
+# ... and the front-end output h0 with them (MARLMAZE_F16_H0=0: fp32 h0)
+F16_H0 = os.environ.get("MARLMAZE_F16_H0", "1") != "0"
 
 
 def _act16(prec, M, widths, next_ks):
@@ -603,13 +605,16 @@ class Actor(nn.Module):
         """x [M, 65] f32 on the GPU -> (head logits z [M, 6], saved state for
         train_backward).  The forward of get_log_probs' actor calls (PPO.py:66-68)."""
         x = x.contiguous()
-        ws, h0 = _front_fwd(x, self.projection.parity_mode, front_params(self.projection, self.attention))
-        if not self._engine(h0):
-            raise ValueError("Actor.train_forward needs the GPU engine's shapes (ReLU, widths <= 272)")
         params = self._mlp_params()
         wl = [lin.weight for lin in self.layers]
-        act16 = (_act16(self.gemm_prec, h0.shape[0], [w_.shape[0] for w_ in wl],
+        act16 = (_act16(self.gemm_prec, x.shape[0], [w_.shape[0] for w_ in wl],
                         [(w_.shape[0], w_.shape[1]) for w_ in wl[1:]]) and (wl[-1].shape[0] + 31) // 32 == 9)
+        # with fp16 activations the front-end output is stored fp16 too (the first GEMM -- the streaming
+        # kernel's fp16 A source at K = 460 -- and its weight gradient round it to fp16 anyway)
+        h16 = act16 and F16_H0 and wl[0].shape[1] % 4 == 0
+        ws, h0 = _front_fwd(x, self.projection.parity_mode, front_params(self.projection, self.attention), h16=h16)
+        if not self._engine(h0):
+            raise ValueError("Actor.train_forward needs the GPU engine's shapes (ReLU, widths <= 272)")
         hs, bits = _mlp_fwd(h0, params[0::2], params[1::2], self.gemm_prec, True, act16=act16)
         w, b = self.heads()
         z = _heads_fwd(hs[-1], w, b)
@@ -646,8 +651,9 @@ def _front_fwd_algo(B):
     return FRONT_FWD_ALGO
 
 
-def _front_fwd(x, parity, params):
-    """The fused front-end forward (no autograd): (workspace, h [B, 460])."""
+def _front_fwd(x, parity, params, h16=False):
+    """The fused front-end forward (no autograd): (workspace, h [B, 460]); h16: h stored fp16
+    (mm_actor_front_fwd_h16, the f16 networks' update: its consumers round h to fp16 anyway)."""
     from . import _lib
 
     from . import x3
@@ -667,6 +673,11 @@ def _front_fwd(x, parity, params):
         return ws
 
     ws = x3.cached_value("front_prep", params, prep)
+    if h16:
+        h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float16, device=x.device)
+        _lib.check(L.mm_actor_front_fwd_h16(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
+                                            stream), "mm_actor_front_fwd_h16")
+        return ws, h
     h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
     _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
                                        _lib.FRONT_FWD[_front_fwd_algo(B)], stream), "mm_actor_front_fwd_ex")

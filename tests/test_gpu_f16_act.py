@@ -76,11 +76,11 @@ def test_f16_train_forward_stores_fp16_and_matches_fp32_storage(monkeypatch):
     x = torch.randn(M, 65, device="cuda")
     z, saved = actor.train_forward(x)
     hs = saved[2]
-    assert hs[0].dtype == torch.float32 and all(h.dtype == torch.float16 for h in hs[1:])
+    assert all(h.dtype == torch.float16 for h in hs)  # the front-end output h0 included (F16_H0)
     monkeypatch.setattr(networks, "F16_ACT", False)
     z32, saved32 = actor.train_forward(x)
     assert all(h.dtype == torch.float32 for h in saved32[2])
-    for h, h32 in zip(hs[1:], saved32[2][1:]):
+    for h, h32 in zip(hs, saved32[2]):
         assert torch.equal(h, h32.half())
     assert torch.equal(z, z32) or (z - z32).abs().max() <= 2e-3 * z32.abs().max()
 
@@ -137,3 +137,29 @@ def test_heads_bwd_fp16_prescaled():
     dy32, cs32 = x3.heads_bwd(dz, w, mb)
     dy16, cs16 = x3.heads_bwd(dz, w, mb, oscale=S)
     assert dy16.dtype == torch.float16 and torch.equal(dy16, (dy32 * S).half()) and torch.equal(cs16, cs32)
+
+
+def test_front_fwd_h16_is_rounded_fp32():
+    torch.manual_seed(8)
+    actor = networks.Actor(hidden_sizes=(264, 264, 264), gemm_prec="f16").cuda()
+    x = torch.randn(3001, 65, device="cuda")
+    params = networks.front_params(actor.projection, actor.attention)
+    _, h32 = networks._front_fwd(x, True, params)
+    _, h16 = networks._front_fwd(x, True, params, h16=True)
+    assert h16.dtype == torch.float16 and torch.equal(h16, h32.half())
+
+
+@pytest.mark.parametrize("M", [M, 3001])
+def test_gemm_fp16_a_k460_streaming_equals_fp32_a(M):
+    """The first trunk layer at K = 460 with fp16 A (the streaming kernel's ASrcF16V; the B-resident kernel
+    does not take that width): equal to the fp32-A form on the same fp16 values, fp16 and fp32 outputs."""
+    g = torch.Generator(device="cuda").manual_seed(M)
+    a16 = torch.randn(M, 460, device="cuda", generator=g).half()
+    w = x3.pack(torch.randn(264, 460, device="cuda", generator=g) * 0.05, prec="f16")
+    b = torch.randn(264, device="cuda", generator=g)
+    mb16, mb32 = x3.mbits(M, "cuda").zero_(), x3.mbits(M, "cuda").zero_()
+    out16 = torch.empty(M, 264, dtype=torch.float16, device="cuda")
+    y16 = x3.gemm(a16, w, bias=b, relu=True, mbits_out=mb16, out=out16)
+    y32 = x3.gemm(a16.float(), w, bias=b, relu=True, mbits_out=mb32)
+    assert torch.equal(y16, y32.half()) and torch.equal(mb16, mb32)
+    assert torch.equal(x3.gemm(a16, w, bias=b, relu=True), y32)
