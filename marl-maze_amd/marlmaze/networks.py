@@ -245,9 +245,10 @@ def _act16(prec, M, widths, next_ks):
 # three ReLU layers without bits (the rollout's trunk) up to this many rows run as ONE launch (mm_trunk3:
 # bit-identical to the per-layer GEMMs below 16,384 rows, where those sit at their launch floor).  Per
 # precision, from tools/bench_trunk.py (profiles/r05_bench_trunk_*.jsonl; fused vs three GEMMs, HIP graphs):
-# x2 8,192 rows 21.8 vs 42.0 us, 49,152 124 vs 133 us; f16 65,536 81 vs 123 us, 131,072 162 vs 259 us.
+# x2 8,192 rows 21.8 vs 42.0 us, 49,152 124 vs 133 us; with the heads + draws (the rollout's form) x2 8,192
+# 25.8 vs 49.1 us but 65,536 196 vs 177 us; f16 65,536 81 vs 123 us, 131,072 162 vs 259 us.
 # MARLMAZE_TRUNK_MAX_ROWS overrides it for every precision (0: off).
-_TRUNK_MAX_ROWS_DEFAULT = {"x2": 49152, "x3": 16384, "f16": 131072}
+_TRUNK_MAX_ROWS_DEFAULT = {"x2": 32768, "x3": 16384, "f16": 131072}
 TRUNK_MAX_ROWS = int(os.environ["MARLMAZE_TRUNK_MAX_ROWS"]) if "MARLMAZE_TRUNK_MAX_ROWS" in os.environ else None
 
 
