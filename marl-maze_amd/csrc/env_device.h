@@ -399,7 +399,7 @@ MM_HD int agent_step(View& v, Agent& a, int move, int mark, uint8_t* gl, uint32_
         const int idx = a.y * v.w + a.x;
         const uint8_t b = (uint8_t)((v.L[idx] & ~3) | a.tag);
         v.L[idx] = b;
-        if (gl) gl[idx] = b;
+        if (gl) __builtin_nontemporal_store(b, gl + idx);  // streaming: no dirty line left for the end-of-kernel release
         a.lmx = a.x;
         a.lmy = a.y;
         a.flags |= MM_AF_HAS_MARK;

@@ -781,8 +781,10 @@ __global__ __launch_bounds__(kStepThreads) void k_step(mm_env_t env, const int8_
     }
     __builtin_nontemporal_store(r, reward + m);
     __builtin_nontemporal_store(dn, done + m);
-    if (ep_stats)  // (episode length, shortest_path_len) of an episode that ended here (PPO.py:129,131)
-        reinterpret_cast<int2*>(ep_stats)[m] = dn ? make_int2(mz.t, mz.path_len) : make_int2(0, 0);
+    if (ep_stats) {  // (episode length, shortest_path_len) of an episode that ended here (PPO.py:129,131)
+        const uint64_t es = dn ? ((uint64_t)(uint32_t)mz.path_len << 32) | (uint32_t)mz.t : 0ull;
+        __builtin_nontemporal_store(es, reinterpret_cast<uint64_t*>(ep_stats) + m);
+    }
     mz.kx = (int8_t)v.kx;
     mz.ky = (int8_t)v.ky;
     mz.status = (uint16_t)status;
