@@ -169,8 +169,8 @@ def _cpu_epoch_bounded(threads, full_batch, max_steps=100, timeout=90):
 
 def cpu_baseline():
     """BASELINE.md's CPU plan: one full train() epoch of
-    the CPU port at the box's CPU share of threads and at 1 thread, and a
-    bounded sample of it at os.cpu_count() threads.  The port's environment is
+    the CPU port at the box's CPU share of threads and at 1 thread (and, with
+    MARLMAZE_CPU_ALL_THREADS=1, a bounded sample at os.cpu_count() threads).  The port's environment is
     the C oracle (bit-exact to the reference's Python env, ~5x faster than it:
     SURVEY §6), its networks / sampling / update are torch-CPU fp32 like the
     reference's, so the figure OVERSTATES the reference's own train() speed."""
@@ -180,7 +180,9 @@ def cpu_baseline():
     for th in (share, 1):
         print(f"cpu baseline: one train() epoch at {th} thread(s)", file=sys.stderr, flush=True)
         runs.append(_cpu_epoch(th))
-    if n_cpu > share:
+    # the os.cpu_count()-thread leg (256 threads in a 16-CPU share: ~0.4 env-steps/s, 90 s of every run in
+    # round 5) is opt-in: MARLMAZE_CPU_ALL_THREADS=1
+    if n_cpu > share and os.environ.get("MARLMAZE_CPU_ALL_THREADS") == "1":
         print(f"cpu baseline: bounded sample at os.cpu_count() = {n_cpu} threads", file=sys.stderr, flush=True)
         runs.append(_cpu_epoch_bounded(n_cpu, runs[1]["_batch"]))
     for r in runs:

@@ -289,6 +289,14 @@ int mm_gemm_nt(int prec, const float* a, int lda, float ascale, const uint16_t* 
 #define MM_GEMM_STREAM 1
 int mm_gemm_nt_algo(int algo);
 long mm_gemm_wgrad_ws_len(int M, int N, int K);
+/* mm_gemm_wgrad_algo: which kernel the MM_PREC_X2 weight gradients of the actor trunk's shapes (264 x 264,
+ * 264 x 460) use (process-wide; returns the previous setting).  MM_WGRAD_DMA: raw rows staged HBM -> LDS by
+ * LDS-DMA into a two-stage ring (two steps in flight); MM_WGRAD_REG: staged through registers one step ahead.
+ * Bit-identical results.  Initial value: MM_WGRAD_REG if the environment sets MARLMAZE_WG_DMA=0, else
+ * MM_WGRAD_DMA.  Replaces nothing in the reference (a kernel choice of networks.py:35-41's backward). */
+#define MM_WGRAD_DMA 0
+#define MM_WGRAD_REG 1
+int mm_gemm_wgrad_algo(int algo);
 int mm_gemm_wgrad(int prec, const float* dy, int lddy, float dscale, const float* x, int ldx, int M, int N, int K,
                   float cscale, float* ws, float* dw, void* stream);
 /* The update's batched forms (one launch for what a backward would otherwise

@@ -1810,6 +1810,231 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     }
 }
 
+// k_wgrad_dma (round 6): k_wgrad_rect<P_X2, TN, NTK> with the staging taken off the registers.  Measured
+// (round 5, 419,430 rows): k_wgrad_rect streams 264 x 264 at 3.1 TB/s and 264 x 460 at 2.6 TB/s.  Its step
+// (32 rows) is ~6.7k cycles against ~1.9k cycles of MFMA per SIMD: each step's pieces are loaded into
+// registers one step ahead (32 VGPRs, all x2 can spare), so one step's bytes (52 KB per CU) are in flight
+// and the step time is the loaded HBM latency.  Here the raw fp32 rows go HBM -> LDS by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no registers), into a ring of TWO raw stages, so two steps' bytes are in
+// flight while the waves run the MFMAs of a third:
+//   LDS = 2 raw stages [A: 32 rows x 16 TN fp32 | B: 32 rows x 16 NTK fp32] + ONE fragment image set
+//   (x2: 156 KB at 17 + 9 tiles); per step: MFMAs from the image; wait for the next stage's DMA; barrier;
+//   every thread converts its pieces of that stage (LDS -> registers -> the image, the x2 split, as
+//   k_wgrad_rect's store_piece); barrier; the freed stage's DMA for the step after next.
+// The DMA (one 1-KiB wave instruction per 64 16-byte pieces; piece p = 64 i + lane of instruction i lands at
+// stage + 16 p) covers row-major [32][16 TN] then [32][16 NTK]: rows past the slice read past the buffer
+// resource's num_records and land as zeros; columns past N / K read finite neighbours, which reach only
+// output rows / columns that are never stored.  Operand rule: a DMA's offset VGPR is
+// not rewritten while the DMA may be in flight -- two offset sets, one per raw stage, each advanced in place
+// only after its previous DMA has been waited for.  The MFMA phase, the partials and the reduction are
+// k_wgrad_rect's (same tile order per output: the same sums, bit for bit).
+constexpr int kWgDmaSets = 2;
+template <int P, int TN, int NTK>
+__global__ __launch_bounds__(kWgThreads) void k_wgrad_dma(const float* __restrict__ dy, int lddy, float dscale,
+                                                          const float* __restrict__ x, int ldx, int M, int N, int K,
+                                                          int rows, int nslices, int ncb, float cscale,
+                                                          float* __restrict__ ws) {
+    static_assert(P == P_X2, "k_wgrad_dma: the x2 weight gradients (fp32 operands)");
+    constexpr int kB = Prec<P>::kBlk;
+    constexpr int np = Prec<P>::kPlanes;
+    constexpr int RN = TN / kWgWaves;
+    constexpr int kRem = (TN - kWgWaves * RN) * NTK;
+    constexpr int EX = (kRem + kWgWaves - 1) / kWgWaves;
+    constexpr int kWA = 16 * TN, kWB = 16 * NTK;           // raw row widths (floats)
+    constexpr int kRaw = 32 * (kWA + kWB);                 // floats per raw stage
+    constexpr int kImg = (TN + NTK) * kB;                  // uint16 per image set
+    constexpr int kInsA = 32 * kWA / 256, kIns = 32 * (kWA + kWB) / 256;  // 1-KiB DMA instructions per stage
+    constexpr int kInsW = (kIns + kWgWaves - 1) / kWgWaves;  // per wave (max)
+    constexpr int kInsWmin = kIns / kWgWaves;                // per wave (min)
+    constexpr int itemsA = 64 * TN, items = itemsA + 64 * NTK;
+    constexpr int kPer = (items + kWgThreads - 1) / kWgThreads;
+    static_assert((2 * kRaw * 4 + kImg * 2) <= 160 * 1024, "LDS");
+    extern __shared__ __attribute__((aligned(16))) uint16_t img[];
+    float* const raw = reinterpret_cast<float*>(img + kImg);  // two stages of kRaw floats
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    const int s = (slot / ncb) * 8 + xcd, cb = slot % ncb;
+    if (s >= nslices) return;  // the whole workgroup
+    const int m_begin = s * rows, nrows = min(M, m_begin + rows) - m_begin;
+    const int col0 = cb * NTK * 16;
+    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(dy + (size_t)m_begin * lddy), (short)0, (int)(nrows * lddy * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + (size_t)m_begin * ldx + col0), (short)0, (int)((nrows * ldx - col0) * 4), 0x00020000);
+
+    // this wave's DMA instructions i = wave + 8 k: the lane's byte offset for the step of each offset set
+    // (set t starts at step t; advanced by two steps, in place, before each later use)
+    uint32_t ob[kWgDmaSets][kInsW];
+#pragma unroll
+    for (int k = 0; k < kInsW; k++) {
+        const int i = wave + kWgWaves * k;
+        const int p = 64 * i + lane;
+        const bool isA = i < kInsA;
+        const int e = isA ? p : p - 32 * kWA / 4;
+        const int w4 = isA ? kWA / 4 : kWB / 4;
+        const int r = e / w4, c4 = e - r * w4;
+        const int ld = isA ? lddy : ldx;
+#pragma unroll
+        for (int t = 0; t < kWgDmaSets; t++) {
+            ob[t][k] = (uint32_t)(((32 * t + r) * ld + 4 * c4) * 4);
+            asm volatile("" : "+v"(ob[t][k]));
+        }
+    }
+    const uint32_t stepA = 2u * 32u * (uint32_t)lddy * 4u, stepB = 2u * 32u * (uint32_t)ldx * 4u;
+    // the DMA of step st into raw stage T = st & 1 with offset set T (T a compile-time index: a runtime index
+    // into ob[][] compiles to a movrel copy into one temporary VGPR per load -- the very rewrite the operand
+    // rule forbids)
+    auto issue_t = [&](auto tc, int st) {
+        constexpr int T = decltype(tc)::value;
+        float* stage = raw + T * kRaw;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < kInsW; k++) {
+            const int i = wave + kWgWaves * k;  // wave-uniform
+            if (i < kIns) {
+                if (st >= 2) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[T][k]) : "s"(i < kInsA ? stepA : stepB));
+#if __has_builtin(__builtin_amdgcn_raw_ptr_buffer_load_lds)  // (the gfx950 pass; the host pass only emits the stub)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(i < kInsA ? rsA : rsB,
+                                                         (__attribute__((address_space(3))) void*)(stage + 256 * i),
+                                                         16, ob[T][k], 0, 0, 0);
+#endif
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto issue = [&](int st) {
+        if (st & 1) issue_t(std::integral_constant<int, 1>{}, st);
+        else issue_t(std::integral_constant<int, 0>{}, st);
+    };
+    // the DMAs of the stage converted next have landed (for this wave): only the later stage's may be in flight
+    auto wait_stage = [&](bool later_in_flight) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (later_in_flight) {
+            if (wave < kIns % kWgWaves || kIns % kWgWaves == 0) {
+                __builtin_amdgcn_s_waitcnt(0x0F70 | (kInsW & 15) | ((kInsW >> 4) << 14));
+            } else {
+                __builtin_amdgcn_s_waitcnt(0x0F70 | (kInsWmin & 15) | ((kInsWmin >> 4) << 14));
+            }
+        } else {
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto barrier = [&]() {  // LDS writes (DMA included: waited above) visible to the workgroup
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // piece q of this thread: (operand, 8-row chunk c, column j) -> its raw words and image destination
+    int rof[kPer], loff[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const int e = threadIdx.x + kWgThreads * q;
+        const bool isA = e < itemsA;
+        const int e2 = isA ? e : e - itemsA, w = isA ? kWA : kWB;
+        const int c = e2 / w, j = e2 - c * w;
+        rof[q] = isA ? 8 * c * kWA + j : 32 * kWA + 8 * c * kWB + j;
+        loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
+    }
+    auto convert = [&](int st) {
+        const float* stage = raw + (st & 1) * kRaw;
+#pragma unroll
+        for (int q = 0; q < kPer; q++) {
+            if (threadIdx.x + kWgThreads * q < items) {
+                const bool isA = threadIdx.x + kWgThreads * q < itemsA;
+                const int w = isA ? kWA : kWB;
+                float v[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) v[i] = stage[rof[q] + i * w];
+                store_piece<P>(v, isA ? dscale : 1.f, reinterpret_cast<uint4*>(img + loff[q]));
+            }
+        }
+    };
+    auto frag = [&](const uint16_t* tile, bf16x8 (&f)[3]) {
+        const bf16x8* p = reinterpret_cast<const bf16x8*>(tile) + lane;
+#pragma unroll
+        for (int q = 0; q < np; q++) f[q] = p[64 * q];
+    };
+
+    f32x4 acc[RN * NTK + EX], accx[RN * NTK + EX];
+#pragma unroll
+    for (int u = 0; u < RN * NTK + EX; u++) acc[u] = accx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nsteps = (nrows + 31) / 32;
+    issue(0);
+    if (nsteps > 1) issue(1);
+    wait_stage(nsteps > 1);
+    barrier();
+    convert(0);
+    barrier();
+    if (nsteps > 2) issue(2);
+    for (int st = 0; st < nsteps; st++) {
+#ifndef WG_NO_MFMA
+        if constexpr (RN > 0) {
+            bf16x8 a[RN][3], b[2][3];
+#pragma unroll
+            for (int r = 0; r < RN; r++) frag(img + (RN * wave + r) * kB, a[r]);
+            frag(img + TN * kB, b[0]);
+#pragma unroll
+            for (int tk = 0; tk < NTK; tk++) {
+                if (tk + 1 < NTK) frag(img + (TN + tk + 1) * kB, b[(tk + 1) & 1]);
+#pragma unroll
+                for (int r = 0; r < RN; r++)
+                    acc[r * NTK + tk] = mma<P>(a[r], b[tk & 1], acc[r * NTK + tk], accx[r * NTK + tk]);
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < EX; e++) {
+            int j = wave + kWgWaves * e;
+            j = j < kRem ? j : kRem - 1;
+            const int tn = kWgWaves * RN + j / NTK, tk = j % NTK;
+            bf16x8 a1[3], b1[3];
+            frag(img + tn * kB, a1);
+            frag(img + (TN + tk) * kB, b1);
+            acc[RN * NTK + e] = mma<P>(a1, b1, acc[RN * NTK + e], accx[RN * NTK + e]);
+        }
+#endif
+        if (st + 1 < nsteps) {
+            wait_stage(st + 2 < nsteps);  // stage st + 1 landed; only stage st + 2's DMAs may be in flight
+            barrier();                    // every wave done with the image; every wave's DMA for st + 1 visible
+            convert(st + 1);
+            barrier();                    // the image holds step st + 1; raw stage (st + 1) & 1 is free
+            if (st + 3 < nsteps) issue(st + 3);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (no DMA outstanding past here: every issued stage was waited for)
+#pragma unroll
+    for (int t = 0; t < kWgDmaSets; t++)
+#pragma unroll
+        for (int k = 0; k < kInsW; k++) asm volatile("" ::"v"(ob[t][k]));
+    uint32_t rm = 0;
+#pragma unroll
+    for (int u = 0; u < RN * NTK + EX; u++) {
+        acc[u] = x2_combine<P>(acc[u], accx[u]);
+        range_acc<P>(rm, acc[u]);
+    }
+    range_note<P>(rm);
+    float* out = ws + (size_t)s * N * K;
+    auto put = [&](const f32x4& v, int tn, int tk) {
+        const int col = col0 + 16 * tk + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const int row = 16 * tn + 4 * (lane >> 4) + g;
+            if (row < N && col < K) out[(size_t)row * K + col] = v[g] * cscale;
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < RN; r++)
+#pragma unroll
+        for (int tk = 0; tk < NTK; tk++) put(acc[r * NTK + tk], RN * wave + r, tk);
+#pragma unroll
+    for (int e = 0; e < EX; e++) {
+        const int j = wave + kWgWaves * e;
+        if (j < kRem) put(acc[RN * NTK + e], kWgWaves * RN + j / NTK, j % NTK);
+    }
+}
+
 // out[e] = sum over the row slices s of ws[s][e]: 16 groups of consecutive slices per element, each group's
 // loads all in flight (the plain per-element loop over S = 256 slices was latency-bound: ~90 us), the
 // groups then summed in order -- a fixed order, so the result is deterministic
@@ -2930,9 +3155,52 @@ static int launch_rect_t(const WgPlan& p, const float* dy, int lddy, float dscal
     return (int)hipGetLastError();
 }
 
+// the DMA-staged x2 kernel (k_wgrad_dma) for the actor trunk's two large shapes; MARLMAZE_WG_DMA=0 keeps
+// k_wgrad_rect (A/B)
+static int g_wgrad_algo = -1;
+static bool wg_dma_enabled() {
+    if (g_wgrad_algo < 0) {
+        const char* e = getenv("MARLMAZE_WG_DMA");
+        g_wgrad_algo = (e && e[0] == '0') ? MM_WGRAD_REG : MM_WGRAD_DMA;
+    }
+    return g_wgrad_algo == MM_WGRAD_DMA;
+}
+
+extern "C" int mm_gemm_wgrad_algo(int algo) {
+    wg_dma_enabled();
+    const int prev = g_wgrad_algo;
+    if (algo == MM_WGRAD_DMA || algo == MM_WGRAD_REG) g_wgrad_algo = algo;
+    return prev;
+}
+
+template <int TN, int NTK>
+static int launch_dma_t(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
+                        int N, int K, float cscale, float* ws, hipStream_t s) {
+    constexpr size_t lds = (size_t)(TN + NTK) * Prec<P_X2>::kBlk * 2 + (size_t)2 * 32 * 16 * (TN + NTK) * 4;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k_wgrad_dma<P_X2, TN, NTK>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024) != hipSuccess)
+            return MM_E_ARG;
+        attr = true;
+    }
+    hipLaunchKernelGGL((k_wgrad_dma<P_X2, TN, NTK>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s, dy,
+                       lddy, dscale, x, ldx, M, N, K, p.rows, p.nslices, p.ncb, cscale, ws);
+    return (int)hipGetLastError();
+}
+
 template <int P, int XB = 4, int AB = 4>
 static int launch_rect_p(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
                          int N, int K, float cscale, float* ws, hipStream_t s) {
+    if constexpr (P == P_X2 && XB == 4 && AB == 4) {
+        // 16-byte pieces: rows and bases 16-byte aligned (else the register-staged kernel)
+        const bool al = (lddy % 4 == 0) && (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(dy) & 15) == 0) &&
+                        ((reinterpret_cast<uintptr_t>(x) & 15) == 0);
+        if (wg_dma_enabled() && al) {
+            if (p.TN == 17 && p.NTK == 9) return launch_dma_t<17, 9>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+            if (p.TN == 17 && p.NTK == 8) return launch_dma_t<17, 8>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);
+        }
+    }
 #define MM_WR(a, b)                                                                                              \
     if (p.TN == a && p.NTK == b)                                                                                 \
         return launch_rect_t<P, a, b, XB, AB>(p, dy, lddy, dscale, x, ldx, M, N, K, cscale, ws, s);

@@ -116,7 +116,8 @@ class PPO:
         # its state is restored afterwards
         g = torch.random.get_rng_state()
         torch.default_generator.manual_seed(seed)
-        # dtype "f32": the networks' GEMMs at fp32-class accuracy (bf16x3 MFMA); "f16": fp16 MFMA operands with
+        # dtype "f32": the networks' GEMMs at fp32-class accuracy (x2 by default: two fp16 planes per operand,
+        # three f16 MFMAs per product, range-guarded; x3 = bf16x3 on request); "f16": fp16 MFMA operands with
         # fp32 accumulation, storage and Adam (BASELINE configs[4]); the parameters are fp32 either way
         if dtype not in ("f32", "f16"):
             raise ValueError(f"dtype must be 'f32' or 'f16', not {dtype!r}")
@@ -184,6 +185,8 @@ class PPO:
         self._graph = None
         self.range_redos = 0  # updates redone at x3 by the range guard (_range_guarded)
         self.range_switched = False  # the rollout's operands left the fp16 range: the networks now run x3
+        self.batches_discarded = 0  # batches the range guard threw away (their rollout left the fp16 range)
+        self.last_update_discarded = False
         self._graph_key = None
         self._graph_warm = False
         self._ctr = None  # device base of the sampler's Philox offset in graph replays
@@ -628,6 +631,7 @@ class PPO:
                 hist /= self.dp.world
             return hist
 
+        self.last_update_discarded = False
         if self.flat is None or self.gemm_prec == "x3":
             return passes()
         return self._range_guarded(passes)
@@ -639,11 +643,22 @@ class PPO:
         self.gemm_prec = self.actor.gemm_prec = self.critic.gemm_prec = prec
         self._graph = None  # a captured rollout holds the old precision's kernels
 
+    def _range_flags(self, pre, post):
+        """(pre_set, post_set) from this rank's two device flags, decided for ALL ranks: under DP the flags
+        are MAX-all-reduced before the one host read, so a range violation on any rank's shard takes every
+        rank down the same branch (the same redo, the same collectives, identical parameters after it)."""
+        flags = torch.cat([pre, post])
+        self.dp.allreduce_max(flags)
+        return tuple(int(v) for v in flags.tolist())  # the synchronisation
+
     def _range_guarded(self, passes):
         """Run the update passes; if any GEMM operand they converted to fp16 planes had |x s| >= 2^15 (the
-        library's range flag, mm_gemm_range_flag), restore the parameters and optimizer state and run the
-        same passes again with the bf16x3 GEMMs (fp32's range).  A flag raised before the update (the
-        rollout's forward GEMMs) switches both networks to x3 from now on.  One host synchronisation per
+        library's range flag, mm_gemm_range_flag) on any rank, restore the parameters and optimizer state and
+        run the same passes again with the bf16x3 GEMMs (fp32's range).  A flag raised before the update (the
+        rollout's actor GEMMs, on any rank) means this batch's actions and old log-probs did not come from the
+        fp32 policy (an inf / NaN accumulator can become 0 through a ReLU): the update on it is thrown away
+        (parameters and optimizer state restored, hist NaN, ``last_update_discarded``), and both networks run
+        their GEMMs at x3 from now on (``train`` then collects a new batch).  One host synchronisation per
         update (the flags' read)."""
         pre = x3.range_flag(clear=True)  # the rollout's conversions since the last update
         flat = self.flat
@@ -651,10 +666,8 @@ class PPO:
         moments = {id(t): t for o in opts for t in (o.exp_avg, o.exp_avg_sq)}
         snap = (flat.data.clone(), {k: t.clone() for k, t in moments.items()}, [o.t for o in opts],
                 [[g["lr"] for g in o.param_groups] for o in opts])
-        hist = passes()
-        post = x3.range_flag(clear=True)
-        pre_set, post_set = (int(v) for v in torch.cat([pre, post]).tolist())  # the synchronisation
-        if post_set:
+
+        def restore():
             with torch.no_grad():
                 flat.data.copy_(snap[0])
                 for k, t in moments.items():
@@ -664,6 +677,23 @@ class PPO:
                 for g, lr in zip(o.param_groups, lrs):
                     g["lr"] = lr
             x3.invalidate_packs()
+
+        hist = passes()
+        post = x3.range_flag(clear=True)
+        pre_set, post_set = self._range_flags(pre, post)
+        self.last_update_discarded = bool(pre_set)
+        if pre_set:
+            restore()
+            warnings.warn(f"marlmaze: a {self.gemm_prec} GEMM operand of the rollout reached |x| >= 2^15 (fp16 "
+                          "planes): the update on this batch is discarded, and both networks run their GEMMs at "
+                          "x3 (bf16x3, fp32 range) from now on")
+            self.set_gemm_prec("x3")
+            self.range_switched = True
+            self.batches_discarded += 1
+            hist.fill_(float("nan"))
+            return hist
+        if post_set:
+            restore()
             prec = self.gemm_prec
             self.set_gemm_prec("x3")
             try:
@@ -671,17 +701,15 @@ class PPO:
             finally:
                 self.set_gemm_prec(prec)
             self.range_redos += 1
-        if pre_set:
-            warnings.warn(f"marlmaze: a {self.gemm_prec} GEMM operand of the rollout reached |x| >= 2^15 (fp16 "
-                          "planes); both networks run their GEMMs at x3 (bf16x3, fp32 range) from now on")
-            self.set_gemm_prec("x3")
-            self.range_switched = True
         return hist
 
     def train(self):
         for epoch in range(self.epochs):
             b_obs, b_act, b_lp, b_sp, ep_lens, b_masks, b_advs, b_vals = self.get_batch()
             hist = self.update(b_obs, b_act, b_lp, b_masks, b_advs, b_vals)
+            if self.last_update_discarded:  # the range guard threw the batch away (now at x3): collect another
+                b_obs, b_act, b_lp, b_sp, ep_lens, b_masks, b_advs, b_vals = self.get_batch()
+                hist = self.update(b_obs, b_act, b_lp, b_masks, b_advs, b_vals)
             episodes, mean_len, mean_short = self.dp.episode_stats(ep_lens, b_sp)  # all ranks' episodes
             stats = dict(epoch=epoch, episodes=episodes, mean_len=mean_len, mean_shortest=mean_short,
                          actor_loss=float(hist[-1, 0]), critic_loss=float(hist[-1, 1]))

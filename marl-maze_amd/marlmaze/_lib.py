@@ -40,7 +40,7 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_actor_front_bwd_to", "mm_actor_front_bwd_grid",
            "mm_x3_tp_len", "mm_x3_tp_pack", "mm_x3_nt", "mm_x3_nt_f32a", "mm_x3_mbits_len",
            "mm_x3_heads_bwd", "mm_ppo_loss_partials", "mm_ppo_loss", "mm_ppo_loss_bwd",
-           "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_ws_len",
+           "mm_gemm_tp_len", "mm_gemm_tp_pack", "mm_gemm_nt", "mm_gemm_nt_algo", "mm_gemm_wgrad_algo", "mm_gemm_wgrad_ws_len",
            "mm_gemm_wgrad", "mm_colsum", "mm_mse_loss_partials", "mm_mse_loss", "mm_losses_final",
            "mm_clip_adam_ws_len", "mm_clip_adam", "mm_gemm_tp_pack_multi", "mm_gemm_wgrad_slices",
            "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi", "mm_critic_value",
@@ -189,6 +189,8 @@ def lib():
         L.mm_gemm_nt.restype = i32
         L.mm_gemm_nt_algo.argtypes = [i32]
         L.mm_gemm_nt_algo.restype = i32
+        L.mm_gemm_wgrad_algo.argtypes = [i32]
+        L.mm_gemm_wgrad_algo.restype = i32
         L.mm_gemm_wgrad_ws_len.argtypes = [i32, i32, i32]
         L.mm_gemm_wgrad_ws_len.restype = ctypes.c_long
         L.mm_gemm_wgrad.argtypes = [i32, P, i32, f32, P, i32, i32, i32, i32, f32, P, P, P]

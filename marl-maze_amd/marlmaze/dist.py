@@ -12,7 +12,10 @@ independent, so rollout and GAE need no communication; the exchange steps are
    the gradient storage (marlmaze.update.FlatParams: no gather or scatter) and
    the 1 / world average is applied inside the optimizer kernel;
 3. per-epoch statistics (episodes finished, their lengths and shortest
-   paths: three fp64 sums, ``episode_stats``).
+   paths: three fp64 sums, ``episode_stats``);
+4. the x2 / f16 range guard's two flags per update (``allreduce_max``), so the
+   decision to redo an update at x3, or to discard a batch, is the same on
+   every rank.
 
 Backend "nccl" is RCCL on ROCm (xGMI inside the node); "gloo" for CPU tests.
 """
@@ -122,6 +125,13 @@ class DP:
     def allreduce_sum(self, t):
         if self.active:
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def allreduce_max(self, t):
+        """In place: the element-wise maximum over ranks (the x2 range guard's flags: a flag raised on any
+        rank is raised on every rank, so all ranks take the same branch and issue the same collectives)."""
+        if self.active:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t
 
     def barrier(self):

@@ -199,6 +199,9 @@ def gemm(a, b, bias=None, relu=False, mbits_in=None, mbits_out=None, colsum=None
     the fp16 range, redo the GEMM at x3 from B's source tensor (pack() records it)."""
     if checked and b.prec != "x3":
         assert b.src is not None, "checked=True needs a TP made by pack()"
+        if a.dtype == torch.float16 or (out is not None and out.dtype == torch.float16) or cscale is not None:
+            # the x3 redo reads fp32 A, writes fp32 and has no output scale: it could not reproduce these
+            raise ValueError("gemm(checked=True) takes fp32 A and output without cscale (the x3 redo's forms)")
         range_flag(clear=True)
         res = gemm(a, b, bias, relu, mbits_in, mbits_out, colsum, ascale, out)
         if int(range_flag(clear=True).item()):
@@ -304,6 +307,17 @@ def set_algo(name):
     return {v: k for k, v in _lib.GEMM_ALGO.items()}[prev]
 
 
+WGRAD_ALGO = {"dma": 0, "reg": 1}  # MM_WGRAD_DMA, MM_WGRAD_REG
+
+
+def set_wgrad_algo(name):
+    """The kernel of the x2 trunk weight gradients (mm_gemm_wgrad_algo, process-wide): "dma" = raw rows
+    staged by LDS-DMA into a two-stage ring (k_wgrad_dma), "reg" = staged through registers (k_wgrad_rect).
+    Bit-identical results.  Returns the previous setting's name."""
+    prev = _lib.lib().mm_gemm_wgrad_algo(WGRAD_ALGO[name])
+    return {v: k for k, v in WGRAD_ALGO.items()}[prev]
+
+
 def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False, cscale=None):
     """dW [N, K] = dY^T X summed over the M rows (mm_gemm_wgrad), dY [M, N] and
     X [M, K] fp32 row-major; fp16 operands take dY * dscale (a power of two).
@@ -311,6 +325,10 @@ def wgrad(dy, x, prec="x3", dscale=1.0, out=None, checked=False, cscale=None):
     sum runs when the scope ends.  checked (x2 / f16): as gemm()'s -- redone at
     x3 when an operand left the fp16 range."""
     if checked and prec != "x3":
+        if dy.dtype == torch.float16 or x.dtype == torch.float16 or cscale is not None:
+            # the x3 redo reads fp32 operands and has no output scale: a pre-scaled fp16 dY would come back
+            # scaled by its s
+            raise ValueError("wgrad(checked=True) takes fp32 dY and X without cscale (the x3 redo's forms)")
         range_flag(clear=True)
         res = wgrad(dy, x, prec, dscale, out)
         if int(range_flag(clear=True).item()):

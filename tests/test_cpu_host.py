@@ -198,6 +198,43 @@ def test_integration_struct_matches_header():
     assert "mm_env_desc_size() == ctypes.sizeof(mm_env_t)" in block
 
 
+_FLAG_WORKER = r"""
+import os, sys, types
+sys.path.insert(0, {pkg!r})
+import torch
+import torch.distributed as dist
+from marlmaze.dist import DP
+from marlmaze.PPO import PPO
+rank, world = int(sys.argv[1]), int(sys.argv[3])
+os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=sys.argv[2])
+dp = DP.from_env(backend="gloo")
+me = types.SimpleNamespace(dp=dp)
+out = []
+for pre_rank, post_rank in ((None, world - 1), (0, None), (None, None), (1, 1)):
+    pre = torch.tensor([int(rank == pre_rank)], dtype=torch.int32)
+    post = torch.tensor([int(rank == post_rank)], dtype=torch.int32)
+    out.append(PPO._range_flags(me, pre, post))
+print("FLAGS", rank, out, flush=True)
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_range_guard_flags_are_collective(tmp_path, world):
+    """PPO._range_flags (the x2 range guard's decision): a flag raised on ONE rank is seen by every rank (MAX
+    all-reduce before the host read), so all ranks redo / discard together and issue the same collectives."""
+    script = str(tmp_path / "flags.py")
+    open(script, "w").write(_FLAG_WORKER.format(pkg=os.path.join(REPO, "marl-maze_amd")))
+    port = str(_free_port())
+    procs = [subprocess.Popen([sys.executable, script, str(r), port, str(world)], stdout=subprocess.PIPE, text=True)
+             for r in range(world)]
+    outs = [p.communicate(timeout=120)[0] for p in procs]
+    assert [p.returncode for p in procs] == [0] * world
+    want = "[(0, 1), (1, 0), (0, 0), (1, 1)]"
+    for r, o in enumerate(outs):
+        assert f"FLAGS {r} {want}" in o, o
+
+
 @pytest.mark.parametrize("world", [2])
 def test_global_advantage_statistics(world):
     from marlmaze.dist import DP

@@ -1,0 +1,136 @@
+"""The x2 range guard under data parallelism (PPO._range_guarded, PPO._range_flags): the redo / discard
+decision is taken from the MAX over ranks of every rank's range flags, so a range violation on ONE rank's
+shard takes every rank down the same branch -- the same collectives, identical parameters afterwards.
+
+Two gloo ranks, one process each, both on cuda:0 (the box has one GPU), on the real GPU update path:
+
+* phase A (post-update flag): only rank 1's batch is scaled past fp16's range (its values x 2^20: the
+  critic's backward GEMM operands leave fp16's range). Both
+  ranks finish, both report ``range_redos == 1``, their parameters and Adam moments are bitwise equal to
+  each other and to the same two-rank update run at x3 from the start (phase B);
+* phase C (pre-update flag): only rank 1 runs an x2 actor forward that leaves fp16's range before an
+  in-range update. Both ranks discard that update (parameters unchanged, hist NaN), both switch to x3, and
+  the next update runs on both without a redo and leaves equal, finite parameters.
+
+Reference: /root/reference/PPO.py:76-85 (the update the guard protects).
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_WORKER = r"""
+import os, sys, warnings
+sys.path.insert(0, {pkg!r}); sys.path.insert(0, {repo!r})
+import torch
+rank = int(sys.argv[1])
+os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                  MASTER_PORT=sys.argv[2])
+from marlmaze.dist import DP
+from marlmaze.PPO import PPO
+from marlmaze import x3
+import torch.distributed as dist
+warnings.simplefilter("ignore")
+dp = DP.from_env(backend="gloo")
+n, T = 256, 16
+B = n * T
+kw = dict(epochs=1, batch_size=2 * (B - B % 5), lr=1.4e-4, n_envs=n, horizon=T, dp=dp, load=False, verbose=False,
+          save=False, bootstrap=False, sample_seed=21,
+          env_config=dict(default_size=(10, 10), max_timestep=40, seed_base=0))
+ag = PPO(2, **kw)
+obs, act, lp, sp, ep_lens, masks, adv, val = ag.get_batch()
+if rank == 1:
+    # only this rank's shard leaves fp16's range: its returns (adv + val) scaled, so the critic's value-loss
+    # gradient dV ~ 2 (V - rtg) / M times the x2 dY scale 2^floor(log2 M) exceeds 2^16 in its backward GEMMs
+    # (the fp32 / x3 arithmetic stays finite: the loss ~1e10, the clipped gradient norm 0.5)
+    val = val * 2.0 ** 20
+idx = torch.randperm(B, generator=torch.Generator().manual_seed(100 + rank)).cuda()
+x3.range_flag(clear=True)
+batch = (obs, act, lp, masks, adv, val)
+
+def state(a):
+    return dict(flat=a.flat.data.cpu(), m=a.actor_optim.exp_avg.cpu(), v=a.actor_optim.exp_avg_sq.cpu(),
+                t=torch.tensor([a.actor_optim.t, a.critic_optim.t]))
+
+# phase A: guarded x2 update
+histA = ag.update(*batch, index_list=idx)
+A = dict(state(ag), hist=histA.cpu(), redos=torch.tensor([ag.range_redos, ag.batches_discarded]),
+         prec=torch.tensor([ag.gemm_prec == "x2"]))
+# phase B: the same update at x3 from the start (a fresh agent: the same initial parameters, seed 3234)
+bg = PPO(2, **kw)
+bg.set_gemm_prec("x3")
+histB = bg.update(*batch, index_list=idx)
+Bs = dict(state(bg), hist=histB.cpu())
+# phase C: a pre-update flag on rank 1 only (an x2 forward out of range), then an in-range update
+cg = PPO(2, **kw)
+in_range = tuple(t.clone() for t in batch)
+if rank == 1:
+    in_range = in_range[:5] + (in_range[5] / 2.0 ** 20,)
+x3.range_flag(clear=True)
+if rank == 1:
+    with torch.no_grad():
+        cg.actor(in_range[0][:512].reshape(1024, 65) * 2.0 ** 17)
+before = cg.flat.data.clone()
+histC = cg.update(*in_range, index_list=idx)
+C = dict(unchanged=torch.tensor([bool(torch.equal(before, cg.flat.data))]), hist=histC.cpu(),
+         flags=torch.tensor([cg.last_update_discarded, cg.batches_discarded, cg.range_switched,
+                             cg.gemm_prec == "x3", cg.range_redos]))
+histC2 = cg.update(*in_range, index_list=idx)
+C.update(flat2=cg.flat.data.cpu(), hist2=histC2.cpu(),
+         flags2=torch.tensor([cg.last_update_discarded, cg.batches_discarded, cg.range_redos]))
+torch.save(dict(A=A, B=Bs, C=C), sys.argv[3] + "_%d.pt" % rank)
+dist.destroy_process_group()
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_range_guard_is_collective_under_dp(tmp_path):
+    script = tmp_path / "worker.py"
+    script.write_text(_WORKER.format(pkg=os.path.join(REPO, "marl-maze_amd"), repo=REPO))
+    out = str(tmp_path / "rank")
+    port = str(_free_port())
+    procs = [subprocess.Popen([sys.executable, "-u", str(script), str(r), port, out], env=dict(os.environ))
+             for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], rcs
+    r = [torch.load(f"{out}_{k}.pt", weights_only=True) for k in range(2)]
+
+    # phase A: both ranks redid the update at x3 (the flag was raised on rank 1 only) and stay on x2
+    for k in range(2):
+        assert r[k]["A"]["redos"].tolist() == [1, 0], (k, r[k]["A"]["redos"])
+        assert bool(r[k]["A"]["prec"][0]), k
+        assert torch.isfinite(r[k]["A"]["flat"]).all(), k
+    for key in ("flat", "m", "v", "t"):
+        assert torch.equal(r[0]["A"][key], r[1]["A"][key]), key  # identical on both ranks
+        for k in range(2):  # = the two-rank update at x3 from the start
+            assert torch.equal(r[k]["A"][key], r[k]["B"][key]), (k, key)
+    assert torch.equal(r[0]["A"]["hist"], r[0]["B"]["hist"])
+
+    # phase C: both ranks discarded the update and switched to x3; the next update runs on both
+    for k in range(2):
+        c = r[k]["C"]
+        assert bool(c["unchanged"][0]), k
+        assert torch.isnan(c["hist"]).all(), k
+        assert c["flags"].tolist() == [1, 1, 1, 1, 0], (k, c["flags"])
+        assert c["flags2"].tolist() == [0, 1, 0], (k, c["flags2"])
+        assert torch.isfinite(c["flat2"]).all() and torch.isfinite(c["hist2"]).all(), k
+    assert torch.equal(r[0]["C"]["flat2"], r[1]["C"]["flat2"])

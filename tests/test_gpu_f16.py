@@ -81,6 +81,53 @@ def test_f16_forward_vs_fp32_oracle(golden, S):
     assert e_logit <= 2e-3 and e_val <= 2e-3, (e_logit, e_val)
 
 
+def test_f16_rollout_forward_65536_rows_vs_fp32_oracle(golden):
+    """configs[4]'s rollout step on one GPU: 32,768 mazes = 65,536 actor rows, which run the fused trunk
+    (k_trunk3, enabled to 131,072 rows at f16) and, in the rollout, the fused trunk + heads + draws.  Both
+    forms' logits against the fp32 oracle actor (oracle.ppo.OActor, the reference's arithmetic) at the
+    bar above: max|got - ref| <= 2e-3 max|ref|."""
+    from marlmaze import networks, ops, x3
+
+    fx = golden("nets")
+    ag = _agent(n_envs=64)
+    actor, critic = _oracle_nets(fx)
+    with torch.no_grad():  # non-trivial heads (see above)
+        actor.move_head.weight.mul_(30.0)
+        actor.mark_head.weight.mul_(30.0)
+    _to_gpu(ag, actor, critic)
+    M = 65536
+    assert M <= networks._trunk_max_rows("f16")
+    g = torch.Generator().manual_seed(65536)
+    obs = torch.as_tensor(fx["obs"]).reshape(-1, 65)
+    obs = obs[torch.arange(M) % obs.shape[0]] * (1 + 0.05 * torch.rand(M, 65, generator=g))  # distinct rows
+    masks = torch.ones(M, 6, dtype=torch.uint8)
+    xg = obs.cuda()
+    with torch.no_grad():
+        ml, kl = ag.actor(xg)  # Actor.logits: the fused trunk at 65,536 rows + the heads
+        got = torch.cat([ml, kl], 1).cpu()
+        h0 = ag.actor._front(xg)
+        params = ag.actor._mlp_params()
+        packs = [x3.pack(w, prec="f16") for w in params[0::2]]
+        assert x3.trunk3_head_sample_ok(M, h0, packs, "f16")
+        hw, hb = ag.actor.heads()
+        act = torch.empty((M, 2), dtype=torch.int8, device="cuda")
+        lg = torch.empty((M, 6), device="cuda")
+        x3.trunk3_head_sample(h0, packs, params[1::2], hw.contiguous(), hb.contiguous(), masks.cuda(), 5, 0, act,
+                              logits=lg)
+        threads = torch.get_num_threads()
+        torch.set_num_threads(min(threads, 16))  # the box's CPU share
+        try:
+            rm, rk = actor(obs)
+        finally:
+            torch.set_num_threads(threads)
+        ref = torch.cat([rm, rk], 1)
+    e_fwd = (got - ref).abs().max().item() / ref.abs().max().item()
+    e_hs = (lg.cpu() - ref).abs().max().item() / ref.abs().max().item()
+    print(f"f16 rollout forward at {M} rows: Actor.logits {e_fwd:.2e}, trunk3_head_sample {e_hs:.2e} of max|ref|")
+    assert e_fwd <= 2e-3 and e_hs <= 2e-3, (e_fwd, e_hs)
+    del ops
+
+
 def test_f16_minibatch_gradients_vs_fp64_oracle(golden):
     fx = golden("nets")
     ag = _agent(n_envs=64)

@@ -201,3 +201,38 @@ def test_x2_range_guard(M, N, K):
     refw = dy.double().t() @ big.double()
     assert _rel_err(dw, refw, dy.double().abs().t() @ big.double().abs()) < TOL["x2"]
     assert int(x3.range_flag().item()) == 0  # the checked forms leave the flag clear
+    # forms the x3 redo cannot reproduce (fp16 operands / output, an output scale) are refused, not redone wrong
+    wf = x3.pack(w, prec="f16")
+    with pytest.raises(ValueError):
+        x3.gemm(a.half(), wf, checked=True)
+    with pytest.raises(ValueError):
+        x3.gemm(a, wf, out=torch.empty((M, N), dtype=torch.float16, device="cuda"), checked=True)
+    with pytest.raises(ValueError):
+        x3.wgrad((dy * s).half(), a, prec="f16", cscale=1.0 / s, checked=True)
+    with pytest.raises(ValueError):
+        x3.wgrad(dy, a.half(), prec="f16", checked=True)
+
+
+@pytest.mark.parametrize("M", [419430, 70001, 3296, 33, 1])
+@pytest.mark.parametrize("N,K", [(264, 264), (264, 460)])
+def test_wgrad_dma_staging_equals_register_staging(M, N, K):
+    """The x2 trunk weight gradients on k_wgrad_dma (raw rows staged by LDS-DMA into a two-stage ring) and
+    on k_wgrad_rect (staged through registers): the same fragment images and MFMA order, so the same
+    partials and sums bit for bit -- at full, ragged (a partial last 32-row step, slices of one step) and
+    strided (lddy / ldx > width) operands -- and the fp32-class bar against fp64."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    big = torch.randn(M, N + 8, device="cuda", generator=g) / max(M, 1)
+    dy = big[:, 4:4 + N]
+    xb = torch.randn(M, K + 12, device="cuda", generator=g)
+    x = xb[:, :K]
+    s = float(2.0 ** int(torch.tensor(float(M)).log2().floor()))
+    prev = x3.set_wgrad_algo("dma")
+    try:
+        d_dma = x3.wgrad(dy, x, prec="x2", dscale=s)
+        x3.set_wgrad_algo("reg")
+        d_reg = x3.wgrad(dy, x, prec="x2", dscale=s)
+    finally:
+        x3.set_wgrad_algo(prev)
+    assert torch.equal(d_dma, d_reg)
+    ref = dy.double().t() @ x.double()
+    assert _rel_err(d_dma, ref, dy.double().abs().t() @ x.double().abs()) < TOL["x2"]

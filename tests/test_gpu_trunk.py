@@ -67,13 +67,68 @@ def test_trunk3_strided_input_and_output_and_no_bias():
     assert bool((out[:, 264:] == 7.0).all())  # nothing written past N
 
 
-def test_trunk3_large_m_matches_b_resident_path():
-    """At >= 16,384 rows the per-layer GEMMs run on k_bres (another k tail form): equal to 1e-6."""
-    g = torch.Generator(device="cuda").manual_seed(11)
-    _, bs, packs = _layers(460, (264, 264, 264), "x2", g)
-    h0 = torch.relu(torch.randn(20000, 460, device="cuda", generator=g))
+# the precision's GEMM bar (tests/test_gpu_gemm.py TOL), relative to the |.|-composition of the three layers
+_GEMM_TOL = {"x3": 1e-6, "x2": 1e-6, "f16": 2e-3}
+
+
+@pytest.mark.parametrize("prec,M", [("x2", 20000), ("x2", 32768), ("x3", 16384), ("f16", 32768), ("f16", 65536),
+                                    ("f16", 131072)])
+def test_trunk3_large_m_matches_b_resident_path(prec, M):
+    """Every row count up to networks._TRUNK_MAX_ROWS_DEFAULT[prec] (x2 32,768, x3 16,384, f16 131,072 --
+    configs[4]'s rollout runs 65,536 rows a step): at >= 16,384 rows the per-layer GEMMs run on k_bres (another
+    k-tail form and accumulation order, so not bit-identical), and the fused trunk equals them at the
+    precision's GEMM bar: |y - y_layers| <= TOL * S3, where S3 = |.|-composition of the three layers
+    (s1 = |h0| |W0|^T + |b0|, s2 = s1 |W1|^T + |b1|, S3 = s2 |W2|^T + |b2|: the bound a per-layer relative
+    error propagates under).  Both are also held to the fp64 composition at 3 x TOL (one rounding per layer)."""
+    assert M <= networks._TRUNK_MAX_ROWS_DEFAULT[prec]
+    g = torch.Generator(device="cuda").manual_seed(11 + M)
+    ws, bs, packs = _layers(460, (264, 264, 264), prec, g)
+    h0 = torch.relu(torch.randn(M, 460, device="cuda", generator=g))
+    assert x3.trunk3_ok(M, h0, packs, prec)
     y, ref = x3.trunk3(h0, packs, bs), _three_gemms(h0, packs, bs)
-    assert (y - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
+    h64, s = h0.double(), h0.double().abs()
+    for w, b in zip(ws, bs):
+        h64 = torch.relu(h64 @ w.double().t() + b.double())
+        s = s @ w.double().abs().t() + b.double().abs()
+    tol = _GEMM_TOL[prec]
+    e_layers = ((y.double() - ref.double()).abs() / s).max().item()
+    e_fused, e_ref = (((t.double() - h64).abs() / s).max().item() for t in (y, ref))
+    print(f"trunk3 {prec} M={M}: fused vs per-layer {e_layers:.2e}, fused vs fp64 {e_fused:.2e}, "
+          f"per-layer vs fp64 {e_ref:.2e} (of S3)")
+    assert e_layers <= tol, e_layers
+    assert e_fused <= 3 * tol and e_ref <= 3 * tol, (e_fused, e_ref)
+
+
+@pytest.mark.parametrize("prec,M", [("x2", 32768), ("f16", 131072)])
+def test_trunk3_head_sample_at_its_row_limit(prec, M):
+    """The rollout's fused form (trunk + heads + draws) at its largest enabled row count: legal actions,
+    log-probs consistent with its own logits (1e-5), logits at the precision's bar against the per-layer
+    GEMMs + the fp32 heads."""
+    from marlmaze import ops
+
+    g = torch.Generator(device="cuda").manual_seed(200 + M)
+    ws, bs, packs = _layers(460, (264, 264, 264), prec, g)
+    hw, hb = _heads(g)
+    h0 = torch.relu(torch.randn(M, 460, device="cuda", generator=g))
+    mk = _masks(M, g)
+    assert x3.trunk3_head_sample_ok(M, h0, packs, prec)
+    act = torch.full((M, 2), -9, dtype=torch.int8, device="cuda")
+    lp, jl, lg = torch.empty(M, device="cuda"), torch.empty(M // 2, device="cuda"), torch.empty(M, 6, device="cuda")
+    x3.trunk3_head_sample(h0, packs, bs, hw, hb, mk, 77, 0, act, lp, jl, logits=lg)
+    ref_h = _three_gemms(h0, packs, bs)
+    ref_lg = ref_h @ hw.t() + hb
+    s = (ref_h.abs() @ hw.abs().t() + hb.abs()).double()
+    assert (((lg.double() - ref_lg.double()).abs()) / s).max().item() <= 3 * _GEMM_TOL[prec]
+    mv = act[:, 0].long()
+    assert bool(((mv >= 0) & (mv < 5)).all()) and bool(mk.gather(1, mv.view(-1, 1)).bool().all())
+    # log-probs from the kernel's own logits (the draw's arithmetic)
+    ml = lg[:, :5].masked_fill(~mk[:, :5].bool(), float("-inf"))
+    want = torch.log_softmax(ml, 1).gather(1, mv.view(-1, 1)).squeeze(1)
+    p = torch.sigmoid(lg[:, 5].masked_fill(~mk[:, 5].bool(), float("-inf")))
+    want = want + torch.log(torch.where(act[:, 1] != 0, p, 1 - p))
+    assert torch.allclose(lp, want, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(jl, lp.view(-1, 2).sum(1), rtol=1e-6, atol=1e-6)
+    del ops
 
 
 def test_actor_trunk_uses_fused_launch_bit_identically(monkeypatch):

@@ -1,4 +1,4 @@
-"""ISA check of k_wgrad_rect's staging loads ("The k_wgrad_rect zeros"): compiles
+"""ISA check of k_wgrad_rect's staging loads (and of k_wgrad_dma's LDS-DMA loads) ("The k_wgrad_rect zeros"): compiles
 csrc/x3mlp.hip for gfx950 and, in every k_wgrad_rect instantiation, collects the operand registers of the
 full-step staging loads (the buffer_load_dword whose VGPR offset the kernel advances in place: that
 VGPR, the SGPR resource, the SGPR offset if any) and lists every instruction from the first such load to the kernel's range-guard epilogue
@@ -37,7 +37,8 @@ def dst(line):
     if not t or t.startswith((";", ".")) or t.endswith(":"):
         return None, set()
     op, _, args = t.partition(" ")
-    if op.startswith(NO_DST) or (op.startswith("v_cmp_") and not op.endswith("_e64")):
+    if op.startswith(NO_DST) or (op.startswith("v_cmp_") and not op.endswith("_e64")) or \
+            (op.startswith("buffer_load") and args.rstrip().endswith(" lds")):  # LDS-DMA: no register destination
         return op, set()
     return op, regs(args.split(",")[0].strip())
 
@@ -51,7 +52,7 @@ def main():
                        stderr=subprocess.DEVNULL)
         asm = open(os.path.join(d, "k.s")).read().split("\n")
     bad = 0
-    starts = [i for i, l in enumerate(asm) if re.match(r"^_ZN2mm2x312k_wgrad_rect.*:", l)]
+    starts = [i for i, l in enumerate(asm) if re.match(r"^_ZN2mm2x3(12k_wgrad_rect|11k_wgrad_dma).*:", l)]
     for s0 in starts:
         name = asm[s0].split(":")[0]
         end = next(i for i in range(s0, len(asm)) if "s_endpgm" in asm[i])
@@ -67,6 +68,11 @@ def main():
             m = re.match(r"\s+buffer_load_dword (v\d+), (v\d+), (s\[\d+:\d+\]), (s\d+|0) offen", l)
             if m and m.group(2) in pinned:
                 for r in regs(m.group(2)) | regs(m.group(3)) | regs(m.group(4)):
+                    first_use.setdefault(r, i)
+            # k_wgrad_dma's LDS-DMA loads (buffer_load_dwordx4 vOFF, s[rsrc], soff offen lds): every one
+            m = re.match(r"\s+buffer_load_dwordx4 (v\d+), (s\[\d+:\d+\]), (s\d+|0) offen lds", l)
+            if m:
+                for r in regs(m.group(1)) | regs(m.group(2)) | regs(m.group(3)):
                     first_use.setdefault(r, i)
         # every staging load has landed by the loop's last barrier (its values were converted and stored before
         # it); hold_operands() keeps the operands live at least that far

@@ -1,6 +1,9 @@
 """k_step statistics from a rocprofv3 kernel trace of bench.py, split by phase.
 
-    python tools/trace_kstep.py TRACE.csv --warmup W --steps K --horizon T [--out summary.json]
+    python tools/trace_kstep.py TRACE.csv --warmup W --steps K --horizon T [--out summary.json] [--rows rows.csv]
+
+TRACE.csv may also be a --rows file written by an earlier run (profiles/ keeps those, so a committed summary
+can be recomputed from the tree).
 
 bench.py runs W warm-up iterations, then K timed ones, each with T env-step
 launches, plus (for graph rollouts) one instrumented rollout afterwards.  The
@@ -18,11 +21,23 @@ import statistics as st
 
 
 def load(path):
+    """(kernel, start, end) rows of a rocprofv3 kernel trace, or of a trimmed --rows file (which keeps the
+    k_step and k_pregen rows only: the summary recomputes from it unchanged)."""
     rows = list(csv.DictReader(open(path)))
     out = []
     for r in rows:
         out.append((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     return out
+
+
+def write_rows(path, ks):
+    """The trimmed trace: only the k_step and k_pregen dispatches, in start order."""
+    keep = sorted([k for k in ks if "k_step" in k[0] or "k_pregen" in k[0]], key=lambda k: k[1])
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Duration_ns"])
+        for n, b, e in keep:
+            w.writerow([n, b, e, e - b])
 
 
 def stats(durs_ns):
@@ -42,8 +57,11 @@ def main():
     ap.add_argument("--mazes", type=int, default=65536)
     ap.add_argument("--alg-bytes", type=int, default=1064)
     ap.add_argument("--out")
+    ap.add_argument("--rows", help="also write the k_step / k_pregen rows of the trace (a CSV this script reads back)")
     a = ap.parse_args()
     ks = load(a.trace)
+    if a.rows:
+        write_rows(a.rows, ks)
     step = sorted([k for k in ks if "k_step" in k[0]], key=lambda k: k[1])
     pregen = [(s, e) for n, s, e in ks if "k_pregen" in n]
 
