@@ -1810,25 +1810,85 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_rect(const float* __restri
     }
 }
 
-// k_wgrad_dma (round 6): k_wgrad_rect<P_X2, TN, NTK> with the staging taken off the registers.  Measured
-// (round 5, 419,430 rows): k_wgrad_rect streams 264 x 264 at 3.1 TB/s and 264 x 460 at 2.6 TB/s.  Its step
-// (32 rows) is ~6.7k cycles against ~1.9k cycles of MFMA per SIMD: each step's pieces are loaded into
-// registers one step ahead (32 VGPRs, all x2 can spare), so one step's bytes (52 KB per CU) are in flight
-// and the step time is the loaded HBM latency.  Here the raw fp32 rows go HBM -> LDS by LDS-DMA
-// (buffer_load_dwordx4 ... lds: no registers), into a ring of TWO raw stages, so two steps' bytes are in
-// flight while the waves run the MFMAs of a third:
-//   LDS = 2 raw stages [A: 32 rows x 16 TN fp32 | B: 32 rows x 16 NTK fp32] + ONE fragment image set
-//   (x2: 156 KB at 17 + 9 tiles); per step: MFMAs from the image; wait for the next stage's DMA; barrier;
-//   every thread converts its pieces of that stage (LDS -> registers -> the image, the x2 split, as
-//   k_wgrad_rect's store_piece); barrier; the freed stage's DMA for the step after next.
-// The DMA (one 1-KiB wave instruction per 64 16-byte pieces; piece p = 64 i + lane of instruction i lands at
-// stage + 16 p) covers row-major [32][16 TN] then [32][16 NTK]: rows past the slice read past the buffer
-// resource's num_records and land as zeros; columns past N / K read finite neighbours, which reach only
-// output rows / columns that are never stored.  Operand rule: a DMA's offset VGPR is
-// not rewritten while the DMA may be in flight -- two offset sets, one per raw stage, each advanced in place
-// only after its previous DMA has been waited for.  The MFMA phase, the partials and the reduction are
-// k_wgrad_rect's (same tile order per output: the same sums, bit for bit).
-constexpr int kWgDmaSets = 2;
+// k_wgrad_dma (round 6): k_wgrad_rect<P_X2, TN, NTK> with the staging taken off the registers and the dY
+// conversion moved under the MFMAs.
+//
+// Why (419,430 rows, 264 x 264; phase-removed builds timed by tools/bench_wgrad_dma.py): k_wgrad_rect takes
+// ~300 us.  Alone, its MFMA phase takes ~96 us (the x2 floor, 3 f16 MFMAs per product), the operand streaming
+// ~132 us (5.3 TB/s) and the conversion to fp16 planes ~71 us; the kernel runs them one after the other per
+// 32-row step, with one step of loads in flight in registers.
+//
+// Here: (1) the raw fp32 rows go HBM -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds) into TWO raw stages,
+// [A: 32 rows x 16 TN][B: 32 rows x 16 NTK] row-major, so two steps' bytes are in flight.  Rows past the
+// slice read past the resource's num_records and land as zeros; columns past N / K read finite neighbours
+// that reach only output rows / columns that are never stored.  (2) One fragment image (k_wgrad_rect's
+// layout).  Its A part (the TN dY tiles, 2/3 of the image) is needed only for the waves' A fragments, which
+// they load into registers at the start of a step (the leftover tiles' one A fragment included); after a
+// barrier the A part is free, and the next step's dY pieces are converted into it between the MFMAs of this
+// step, which read only the B part.  The X pieces (1/3) are converted after the MFMAs.  Per step: A
+// fragments; [wait for this wave's DMAs of the next step; barrier]; MFMAs + the dY conversion; barrier; the X
+// conversion; barrier; the freed raw stage takes the DMA of the step after next.
+//
+// The DMA is inline asm (dma16): the compiler then sees no LDS write it cannot place, and inserts none of
+// its own vmcnt waits before LDS accesses (through the stage pointers it made every conversion wait for
+// every DMA in flight: vmcnt(0), one step of prefetch).  The kernel waits for its DMAs itself, by count.
+// Operand rule: an in-flight DMA's offset VGPR is never rewritten (one offset set per
+// raw stage, advanced in place by two steps after its previous DMA was waited for); its resource SGPRs are
+// held for the whole kernel.  The MFMA order per output tile and the images are k_wgrad_rect's: the same
+// partials, bit for bit.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t lds) {
+    uint32_t save;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "v"(voff), "s"(r), "s"(lds)
+                 : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// pair2 (x s -> the x2 (hi, lo) fp16 pair of two values) in NON-packed instructions, for conversions that
+// run beside MFMAs: packed f32 VALU (v_pk_mul_f32 / v_pk_fma_f32, which the compiler SLP-forms from pair2's
+// vector arithmetic) costs ~22-26 extra cycles per instruction next to an MFMA (MI355X_MICROARCH.md), plain
+// VOP3 / VOP3P-mix instructions do not.  Same values as pair2: hi = RN16(x s); x s - hi exactly by one
+// v_fma_mix_f32 reading hi's halves (x s is exact, s a power of two; the difference is exact, Sterbenz);
+// times 2^11 exactly; RN16.  SCALED = false: s = 1 (no multiplies).
+template <bool SCALED>
+__device__ __forceinline__ void pair2_plain(float x0, float x1, float s, uint32_t& h, uint32_t& l) {
+    float y0, y1;
+    if constexpr (SCALED) {
+        asm("v_mul_f32 %0, %4, %6\n\t"
+            "v_mul_f32 %1, %5, %6\n\t"
+            "v_cvt_pk_f16_f32 %2, %0, %1\n\t"
+            "v_fma_mix_f32 %0, %4, %6, -%2 op_sel_hi:[0,0,1]\n\t"
+            "v_fma_mix_f32 %1, %5, %6, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+            "v_mul_f32 %0, 0x45000000, %0\n\t"
+            "v_mul_f32 %1, 0x45000000, %1\n\t"
+            "v_cvt_pk_f16_f32 %3, %0, %1"
+            : "=&v"(y0), "=&v"(y1), "=&v"(h), "=&v"(l)
+            : "v"(x0), "v"(x1), "v"(s));
+    } else {
+        asm("v_cvt_pk_f16_f32 %2, %4, %5\n\t"
+            "v_fma_mix_f32 %0, %4, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+            "v_fma_mix_f32 %1, %5, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+            "v_mul_f32 %0, 0x45000000, %0\n\t"
+            "v_mul_f32 %1, 0x45000000, %1\n\t"
+            "v_cvt_pk_f16_f32 %3, %0, %1"
+            : "=&v"(y0), "=&v"(y1), "=&v"(h), "=&v"(l)
+            : "v"(x0), "v"(x1));
+        (void)s;
+    }
+}
+template <bool SCALED>
+__device__ __forceinline__ void store_piece_x2_plain(const float* v, float s, uint4* dst) {
+    uint32_t hh[4], ll[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) pair2_plain<SCALED>(v[2 * k], v[2 * k + 1], s, hh[k], ll[k]);
+    dst[0] = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+    dst[64] = make_uint4(ll[0], ll[1], ll[2], ll[3]);
+}
+
 template <int P, int TN, int NTK>
 __global__ __launch_bounds__(kWgThreads) void k_wgrad_dma(const float* __restrict__ dy, int lddy, float dscale,
                                                           const float* __restrict__ x, int ldx, int M, int N, int K,
@@ -1840,17 +1900,19 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_dma(const float* __restric
     constexpr int RN = TN / kWgWaves;
     constexpr int kRem = (TN - kWgWaves * RN) * NTK;
     constexpr int EX = (kRem + kWgWaves - 1) / kWgWaves;
-    constexpr int kWA = 16 * TN, kWB = 16 * NTK;           // raw row widths (floats)
-    constexpr int kRaw = 32 * (kWA + kWB);                 // floats per raw stage
-    constexpr int kImg = (TN + NTK) * kB;                  // uint16 per image set
-    constexpr int kInsA = 32 * kWA / 256, kIns = 32 * (kWA + kWB) / 256;  // 1-KiB DMA instructions per stage
+    static_assert(RN > 0 && (kRem == 0 || TN - kWgWaves * RN == 1), "leftover tiles of one n-tile (one A fragment)");
+    constexpr int kWA = 16 * TN, kWB = 16 * NTK;            // raw row widths (floats)
+    constexpr int kRawA = 32 * kWA, kRaw = 32 * (kWA + kWB);  // floats
+    constexpr int kImg = (TN + NTK) * kB;                   // uint16 per image
+    constexpr int kInsA = kRawA / 256, kIns = kRaw / 256;   // 1-KiB DMA instructions per stage
     constexpr int kInsW = (kIns + kWgWaves - 1) / kWgWaves;  // per wave (max)
     constexpr int kInsWmin = kIns / kWgWaves;                // per wave (min)
-    constexpr int itemsA = 64 * TN, items = itemsA + 64 * NTK;
-    constexpr int kPer = (items + kWgThreads - 1) / kWgThreads;
+    constexpr int itemsA = 64 * TN, itemsB = 64 * NTK;
+    constexpr int kPerA = (itemsA + kWgThreads - 1) / kWgThreads, kPerB = (itemsB + kWgThreads - 1) / kWgThreads;
     static_assert((2 * kRaw * 4 + kImg * 2) <= 160 * 1024, "LDS");
-    extern __shared__ __attribute__((aligned(16))) uint16_t img[];
-    float* const raw = reinterpret_cast<float*>(img + kImg);  // two stages of kRaw floats
+    __shared__ __attribute__((aligned(16))) float raw0[kRaw];
+    __shared__ __attribute__((aligned(16))) float raw1[kRaw];
+    __shared__ __attribute__((aligned(16))) uint16_t img[kImg];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
@@ -1858,57 +1920,51 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_dma(const float* __restric
     if (s >= nslices) return;  // the whole workgroup
     const int m_begin = s * rows, nrows = min(M, m_begin + rows) - m_begin;
     const int col0 = cb * NTK * 16;
-    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+    __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(dy + (size_t)m_begin * lddy), (short)0, (int)(nrows * lddy * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+    __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(x + (size_t)m_begin * ldx + col0), (short)0, (int)((nrows * ldx - col0) * 4), 0x00020000);
+    asm volatile("" : "+s"(rsA));
+    asm volatile("" : "+s"(rsB));
 
-    // this wave's DMA instructions i = wave + 8 k: the lane's byte offset for the step of each offset set
-    // (set t starts at step t; advanced by two steps, in place, before each later use)
-    uint32_t ob[kWgDmaSets][kInsW];
+    // this wave's DMA instructions i = wave + 8 k: the lane's byte offset in the step of each offset set
+    uint32_t ob[2][kInsW];
 #pragma unroll
     for (int k = 0; k < kInsW; k++) {
         const int i = wave + kWgWaves * k;
         const int p = 64 * i + lane;
         const bool isA = i < kInsA;
-        const int e = isA ? p : p - 32 * kWA / 4;
+        const int e = isA ? p : p - kRawA / 4;
         const int w4 = isA ? kWA / 4 : kWB / 4;
         const int r = e / w4, c4 = e - r * w4;
         const int ld = isA ? lddy : ldx;
 #pragma unroll
-        for (int t = 0; t < kWgDmaSets; t++) {
+        for (int t = 0; t < 2; t++) {
             ob[t][k] = (uint32_t)(((32 * t + r) * ld + 4 * c4) * 4);
             asm volatile("" : "+v"(ob[t][k]));
         }
     }
     const uint32_t stepA = 2u * 32u * (uint32_t)lddy * 4u, stepB = 2u * 32u * (uint32_t)ldx * 4u;
-    // the DMA of step st into raw stage T = st & 1 with offset set T (T a compile-time index: a runtime index
-    // into ob[][] compiles to a movrel copy into one temporary VGPR per load -- the very rewrite the operand
-    // rule forbids)
-    auto issue_t = [&](auto tc, int st) {
+    auto issue = [&](auto tc, int st) {  // the DMA of step st into raw stage T (offset set T)
         constexpr int T = decltype(tc)::value;
-        float* stage = raw + T * kRaw;
+#ifdef WG_NO_DMA  // diagnostic builds only (wrong results): no loads
+        return;
+#endif
+        const uint32_t base = lds_addr(T ? raw1 : raw0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < kInsW; k++) {
             const int i = wave + kWgWaves * k;  // wave-uniform
             if (i < kIns) {
                 if (st >= 2) asm volatile("v_add_u32 %0, %0, %1" : "+v"(ob[T][k]) : "s"(i < kInsA ? stepA : stepB));
-#if __has_builtin(__builtin_amdgcn_raw_ptr_buffer_load_lds)  // (the gfx950 pass; the host pass only emits the stub)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(i < kInsA ? rsA : rsB,
-                                                         (__attribute__((address_space(3))) void*)(stage + 256 * i),
-                                                         16, ob[T][k], 0, 0, 0);
-#endif
+                dma16(i < kInsA ? rsA : rsB, ob[T][k], base + 1024u * (uint32_t)i);
             }
         }
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto issue = [&](int st) {
-        if (st & 1) issue_t(std::integral_constant<int, 1>{}, st);
-        else issue_t(std::integral_constant<int, 0>{}, st);
-    };
-    // the DMAs of the stage converted next have landed (for this wave): only the later stage's may be in flight
+    // this wave's DMAs of the stage converted next have landed; only the later stage's may be in flight
     auto wait_stage = [&](bool later_in_flight) {
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         if (later_in_flight) {
             if (wave < kIns % kWgWaves || kIns % kWgWaves == 0) {
@@ -1920,36 +1976,43 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_dma(const float* __restric
             __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
         }
         __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
     };
-    auto barrier = [&]() {  // LDS writes (DMA included: waited above) visible to the workgroup
+    auto barrier = [&]() {  // LDS writes visible to the workgroup (the DMAs: waited for above)
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt((15 << 0) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
-    // piece q of this thread: (operand, 8-row chunk c, column j) -> its raw words and image destination
-    int rof[kPer], loff[kPer];
+    // piece q of an operand: (8-row chunk c, column j) of this thread -> its raw words and image destination
+    auto piece_conv = [&](const float* stage, bool isA, int e) {
+#ifdef WG_NO_CONV  // diagnostic builds only (wrong results): no conversion
+        return;
+#endif
+        const int w = isA ? kWA : kWB;
+        const int c = e / w, j = e - c * w;
+        const float* src = stage + (isA ? 0 : kRawA) + 8 * c * w + j;
+        float v[8];
 #pragma unroll
-    for (int q = 0; q < kPer; q++) {
+        for (int i = 0; i < 8; i++) v[i] = src[i * w];
+        const int loff = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
+#ifdef WG_PACKED_CONV  // A/B: the packed-f32 form (store_piece)
+        store_piece<P>(v, isA ? dscale : 1.f, reinterpret_cast<uint4*>(img + loff));
+#else
+        if (isA) store_piece_x2_plain<true>(v, dscale, reinterpret_cast<uint4*>(img + loff));
+        else store_piece_x2_plain<false>(v, 1.f, reinterpret_cast<uint4*>(img + loff));
+#endif
+    };
+    auto convA = [&](const float* stage, int q) {
         const int e = threadIdx.x + kWgThreads * q;
-        const bool isA = e < itemsA;
-        const int e2 = isA ? e : e - itemsA, w = isA ? kWA : kWB;
-        const int c = e2 / w, j = e2 - c * w;
-        rof[q] = isA ? 8 * c * kWA + j : 32 * kWA + 8 * c * kWB + j;
-        loff[q] = (isA ? 0 : TN * kB) + (j >> 4) * kB + c * 128 + (j & 15) * 8;
-    }
-    auto convert = [&](int st) {
-        const float* stage = raw + (st & 1) * kRaw;
+        if (e < itemsA) piece_conv(stage, true, e);
+    };
+    auto convB = [&](const float* stage) {
 #pragma unroll
-        for (int q = 0; q < kPer; q++) {
-            if (threadIdx.x + kWgThreads * q < items) {
-                const bool isA = threadIdx.x + kWgThreads * q < itemsA;
-                const int w = isA ? kWA : kWB;
-                float v[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) v[i] = stage[rof[q] + i * w];
-                store_piece<P>(v, isA ? dscale : 1.f, reinterpret_cast<uint4*>(img + loff[q]));
-            }
+        for (int q = 0; q < kPerB; q++) {
+            const int e = threadIdx.x + kWgThreads * q;
+            if (e < itemsB) piece_conv(stage, false, e);
         }
     };
     auto frag = [&](const uint16_t* tile, bf16x8 (&f)[3]) {
@@ -1962,52 +2025,90 @@ __global__ __launch_bounds__(kWgThreads) void k_wgrad_dma(const float* __restric
 #pragma unroll
     for (int u = 0; u < RN * NTK + EX; u++) acc[u] = accx[u] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nsteps = (nrows + 31) / 32;
-    issue(0);
-    if (nsteps > 1) issue(1);
+    constexpr std::integral_constant<int, 0> c0{};
+    constexpr std::integral_constant<int, 1> c1{};
+    issue(c0, 0);
+    if (nsteps > 1) issue(c1, 1);
     wait_stage(nsteps > 1);
     barrier();
-    convert(0);
+#pragma unroll
+    for (int q = 0; q < kPerA; q++) convA(raw0, q);
+    convB(raw0);
     barrier();
-    if (nsteps > 2) issue(2);
-    for (int st = 0; st < nsteps; st++) {
+    if (nsteps > 2) issue(c0, 2);
+    // WG_SPLIT_CONV=1: the dY pieces of the next step go between the MFMAs (piece q after k-tile kAtStride (q +
+    // 1) - 1), the image's A part freed by a barrier after the A fragments are loaded.  Measured (419,430 rows):
+    // 264 x 264 296-300 us against 282 us with the whole conversion after the MFMAs (0, the default); 264 x 460
+    // 465 against 467 -- the conversion's VALU did not hide under the MFMAs (non-packed instructions or not)
+#ifndef WG_SPLIT_CONV
+#define WG_SPLIT_CONV 0
+#endif
+    constexpr bool kSplit = WG_SPLIT_CONV != 0;
+    constexpr int kAtStride = NTK / (kPerA + 1) > 0 ? NTK / (kPerA + 1) : 1;
+    auto step = [&](auto tc, int st) {  // step st; raw stage 1 - T holds step st + 1 (T = st & 1)
+        constexpr int T = decltype(tc)::value;
+        constexpr std::integral_constant<int, 1 - T> cn{};
+        const float* nxt = T ? raw0 : raw1;
+        const bool more = st + 1 < nsteps;
+        bf16x8 a[RN][3], ax[3], b[2][3];
+#pragma unroll
+        for (int r = 0; r < RN; r++) frag(img + (RN * wave + r) * kB, a[r]);
+        if constexpr (EX > 0) frag(img + kWgWaves * RN * kB, ax);  // the leftover tiles' n-tile
+        frag(img + TN * kB, b[0]);
+        if constexpr (kSplit) {
+            if (more) wait_stage(st + 2 < nsteps);  // step st + 1's DMAs (this wave) landed
+            barrier();  // every wave holds its A fragments: the image's A part is free; step st + 1's raw visible
+        }
 #ifndef WG_NO_MFMA
-        if constexpr (RN > 0) {
-            bf16x8 a[RN][3], b[2][3];
 #pragma unroll
-            for (int r = 0; r < RN; r++) frag(img + (RN * wave + r) * kB, a[r]);
-            frag(img + TN * kB, b[0]);
+        for (int tk = 0; tk < NTK; tk++) {
+            if (tk + 1 < NTK) frag(img + (TN + tk + 1) * kB, b[(tk + 1) & 1]);
 #pragma unroll
-            for (int tk = 0; tk < NTK; tk++) {
-                if (tk + 1 < NTK) frag(img + (TN + tk + 1) * kB, b[(tk + 1) & 1]);
+            for (int r = 0; r < RN; r++)
+                acc[r * NTK + tk] = mma<P>(a[r], b[tk & 1], acc[r * NTK + tk], accx[r * NTK + tk]);
+            if constexpr (kSplit) {
 #pragma unroll
-                for (int r = 0; r < RN; r++)
-                    acc[r * NTK + tk] = mma<P>(a[r], b[tk & 1], acc[r * NTK + tk], accx[r * NTK + tk]);
+                for (int q = 0; q < kPerA; q++)
+                    if (tk == kAtStride * (q + 1) - 1 && more) convA(nxt, q);
             }
         }
 #pragma unroll
         for (int e = 0; e < EX; e++) {
             int j = wave + kWgWaves * e;
             j = j < kRem ? j : kRem - 1;
-            const int tn = kWgWaves * RN + j / NTK, tk = j % NTK;
-            bf16x8 a1[3], b1[3];
-            frag(img + tn * kB, a1);
+            const int tk = j % NTK;
+            bf16x8 b1[3];
             frag(img + (TN + tk) * kB, b1);
-            acc[RN * NTK + e] = mma<P>(a1, b1, acc[RN * NTK + e], accx[RN * NTK + e]);
+            acc[RN * NTK + e] = mma<P>(ax, b1, acc[RN * NTK + e], accx[RN * NTK + e]);
+        }
+#else
+        if (more && kSplit) {
+#pragma unroll
+            for (int q = 0; q < kPerA; q++) convA(nxt, q);
         }
 #endif
-        if (st + 1 < nsteps) {
-            wait_stage(st + 2 < nsteps);  // stage st + 1 landed; only stage st + 2's DMAs may be in flight
-            barrier();                    // every wave done with the image; every wave's DMA for st + 1 visible
-            convert(st + 1);
-            barrier();                    // the image holds step st + 1; raw stage (st + 1) & 1 is free
-            if (st + 3 < nsteps) issue(st + 3);
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // (no DMA outstanding past here: every issued stage was waited for)
+        if (more) {
+            if constexpr (!kSplit) wait_stage(st + 2 < nsteps);  // step st + 1's DMAs (this wave) landed
+            barrier();  // the MFMAs' reads of the image are done (and, unsplit, step st + 1's raw is visible)
+            if constexpr (!kSplit) {
 #pragma unroll
-    for (int t = 0; t < kWgDmaSets; t++)
+                for (int q = 0; q < kPerA; q++) convA(nxt, q);
+            }
+            convB(nxt);
+            barrier();  // the image holds step st + 1; raw stage 1 - T is free
+            if (st + 3 < nsteps) issue(cn, st + 3);
+        }
+    };
+    for (int st = 0; st < nsteps; st += 2) {
+        step(c0, st);
+        if (st + 1 < nsteps) step(c1, st + 1);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // (every issued DMA was waited for before its conversion)
+#pragma unroll
+    for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int k = 0; k < kInsW; k++) asm volatile("" ::"v"(ob[t][k]));
+    asm volatile("" ::"s"(rsA), "s"(rsB), "s"(stepA), "s"(stepB));
     uint32_t rm = 0;
 #pragma unroll
     for (int u = 0; u < RN * NTK + EX; u++) {
@@ -3176,15 +3277,7 @@ extern "C" int mm_gemm_wgrad_algo(int algo) {
 template <int TN, int NTK>
 static int launch_dma_t(const WgPlan& p, const float* dy, int lddy, float dscale, const float* x, int ldx, int M,
                         int N, int K, float cscale, float* ws, hipStream_t s) {
-    constexpr size_t lds = (size_t)(TN + NTK) * Prec<P_X2>::kBlk * 2 + (size_t)2 * 32 * 16 * (TN + NTK) * 4;
-    static bool attr = false;
-    if (!attr) {
-        if (hipFuncSetAttribute((const void*)k_wgrad_dma<P_X2, TN, NTK>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess)
-            return MM_E_ARG;
-        attr = true;
-    }
-    hipLaunchKernelGGL((k_wgrad_dma<P_X2, TN, NTK>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), lds, s, dy,
+    hipLaunchKernelGGL((k_wgrad_dma<P_X2, TN, NTK>), dim3(rup(p.nslices, 8) * p.ncb), dim3(kWgThreads), 0, s, dy,
                        lddy, dscale, x, ldx, M, N, K, p.rows, p.nslices, p.ncb, cscale, ws);
     return (int)hipGetLastError();
 }
