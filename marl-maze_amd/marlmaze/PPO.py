@@ -187,6 +187,7 @@ class PPO:
         self.range_switched = False  # the rollout's operands left the fp16 range: the networks now run x3
         self.batches_discarded = 0  # batches the range guard threw away (their rollout left the fp16 range)
         self.last_update_discarded = False
+        self._flag_armed = False  # a rollout cleared the range flag at its start: the next update reads its flag
         self._graph_key = None
         self._graph_warm = False
         self._ctr = None  # device base of the sampler's Philox offset in graph replays
@@ -236,9 +237,17 @@ class PPO:
     # ------------------------------------------------------------------
     # rollout (PPO.get_batch, PPO.py:89-152)
     # ------------------------------------------------------------------
+    def _arm_range_flag(self):
+        """A rollout starts: clear the library's range flag, so that what the next update reads as the
+        rollout's flag (``pre``, _range_guarded) covers this batch's GEMMs and nothing older."""
+        if self.flat is not None and self.gemm_prec != "x3":
+            x3.range_flag(clear=True)
+            self._flag_armed = True
+
     @torch.no_grad()
     def rollout(self):
         """Advance every maze ``horizon`` steps; fills the [T, N] buffers."""
+        self._arm_range_flag()
         self._ensure_env()
         b, n, T = self._bufs, self.n_envs, self.horizon
         if self.graph_rollout and self.step_events is None and self.device.type == "cuda":
@@ -382,6 +391,7 @@ class PPO:
         sampler's Philox offset carry any trace of the overshoot into the next
         batch.
         """
+        self._arm_range_flag()
         self._ensure_env()
         n, dev = self.n_envs, self.device
         limit = self.batch_size // self.dp.world
@@ -654,13 +664,18 @@ class PPO:
     def _range_guarded(self, passes):
         """Run the update passes; if any GEMM operand they converted to fp16 planes had |x s| >= 2^15 (the
         library's range flag, mm_gemm_range_flag) on any rank, restore the parameters and optimizer state and
-        run the same passes again with the bf16x3 GEMMs (fp32's range).  A flag raised before the update (the
-        rollout's actor GEMMs, on any rank) means this batch's actions and old log-probs did not come from the
+        run the same passes again with the bf16x3 GEMMs (fp32's range).  A flag raised since the batch's rollout
+        began (its actor GEMMs, on any rank) means this batch's actions and old log-probs did not come from the
         fp32 policy (an inf / NaN accumulator can become 0 through a ReLU): the update on it is thrown away
         (parameters and optimizer state restored, hist NaN, ``last_update_discarded``), and both networks run
         their GEMMs at x3 from now on (``train`` then collects a new batch).  One host synchronisation per
         update (the flags' read)."""
-        pre = x3.range_flag(clear=True)  # the rollout's conversions since the last update
+        # the flag raised since this agent's last rollout began (its actor GEMMs); a batch that did not come
+        # from a rollout of this agent (update() on given tensors) has no rollout flag: a stale one is dropped
+        pre = x3.range_flag(clear=True)
+        if not self._flag_armed:
+            pre.zero_()
+        self._flag_armed = False
         flat = self.flat
         opts = (self.actor_optim, self.critic_optim)
         moments = {id(t): t for o in opts for t in (o.exp_avg, o.exp_avg_sq)}

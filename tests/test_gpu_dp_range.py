@@ -8,8 +8,8 @@ Two gloo ranks, one process each, both on cuda:0 (the box has one GPU), on the r
   critic's backward GEMM operands leave fp16's range). Both
   ranks finish, both report ``range_redos == 1``, their parameters and Adam moments are bitwise equal to
   each other and to the same two-rank update run at x3 from the start (phase B);
-* phase C (pre-update flag): only rank 1 runs an x2 actor forward that leaves fp16's range before an
-  in-range update. Both ranks discard that update (parameters unchanged, hist NaN), both switch to x3, and
+* phase C (rollout flag): after a rollout on both ranks, only rank 1 runs an x2 actor forward that leaves
+  fp16's range before an in-range update. Both ranks discard that update (parameters unchanged, hist NaN), both switch to x3, and
   the next update runs on both without a redo and leaves equal, finite parameters.
 
 Reference: /root/reference/PPO.py:76-85 (the update the guard protects).
@@ -68,12 +68,13 @@ bg = PPO(2, **kw)
 bg.set_gemm_prec("x3")
 histB = bg.update(*batch, index_list=idx)
 Bs = dict(state(bg), hist=histB.cpu())
-# phase C: a pre-update flag on rank 1 only (an x2 forward out of range), then an in-range update
+# phase C: a rollout-window flag on rank 1 only (after its rollout, an x2 actor forward out of range), then
+# an in-range update
 cg = PPO(2, **kw)
 in_range = tuple(t.clone() for t in batch)
 if rank == 1:
     in_range = in_range[:5] + (in_range[5] / 2.0 ** 20,)
-x3.range_flag(clear=True)
+cg.get_batch()  # (its rollout opens the window the next update reads as the rollout's flag)
 if rank == 1:
     with torch.no_grad():
         cg.actor(in_range[0][:512].reshape(1024, 65) * 2.0 ** 17)

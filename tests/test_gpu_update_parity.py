@@ -518,3 +518,50 @@ def test_update_range_guard_redoes_at_x3(golden):
     _to_gpu(ag, actor2, critic2)
     ag.update(obs, act, old, masks, adv, vals, index_list=torch.arange(S))
     assert ag.range_redos == 0 and ag.gemm_prec == "x2" and torch.isfinite(ag.flat.data).all()
+
+
+def test_rollout_range_flag_discards_the_batch():
+    """A rollout whose x2 actor GEMMs left fp16's range (the trunk's first-layer weights x 2^17: its hidden
+    activations pass 2^16) raises the library's range flag.  The update on that batch is thrown away -- its
+    actions and old log-probs did not come from the fp32 policy -- so the parameters and the Adam state are
+    unchanged and hist is NaN; both networks run at x3 from then on, and the next batch (collected at x3)
+    trains normally: no redo, finite parameters.  ``train()`` does both in one epoch.  A stale flag from
+    GEMMs outside this agent's rollouts (update() on given tensors) is not a rollout flag."""
+    from marlmaze import x3
+
+    n, T = 64, 16
+    kw = dict(n_envs=n, horizon=T, batch_size=n * T, epochs=1, sample_seed=9, bootstrap=False,
+              env_config=dict(default_size=(10, 10), max_timestep=40, seed_base=0))
+    ag = _agent(**kw)
+    with torch.no_grad():
+        ag.actor.layers[0].weight.mul_(2.0 ** 17)
+    x3.invalidate_packs()
+    batch = ag.get_batch()
+    before = ag.flat.data.clone()
+    m_before = ag.actor_optim.exp_avg.clone()
+    hist = ag.update(batch[0], batch[1], batch[2], batch[5], batch[6], batch[7])
+    torch.cuda.synchronize()
+    assert ag.last_update_discarded and ag.batches_discarded == 1 and ag.range_switched
+    assert ag.gemm_prec == "x3" and ag.actor.gemm_prec == "x3" and ag.critic.gemm_prec == "x3"
+    assert torch.isnan(hist).all()
+    assert torch.equal(ag.flat.data, before) and torch.equal(ag.actor_optim.exp_avg, m_before)
+    assert ag.actor_optim.t == 0
+    batch = ag.get_batch()
+    hist = ag.update(batch[0], batch[1], batch[2], batch[5], batch[6], batch[7])
+    assert not ag.last_update_discarded and ag.range_redos == 0 and ag.batches_discarded == 1
+    K = hist.shape[0]  # minibatch steps of one update (Q8: 6 x 5 here)
+    assert torch.isfinite(hist).all() and torch.isfinite(ag.flat.data).all() and ag.actor_optim.t == K
+    # train(): the discarded batch is re-collected inside the epoch
+    bg = _agent(**kw)
+    with torch.no_grad():
+        bg.actor.layers[0].weight.mul_(2.0 ** 17)
+    x3.invalidate_packs()
+    bg.train()
+    assert bg.batches_discarded == 1 and bg.actor_optim.t == K and np.isfinite(bg.history[-1]["actor_loss"])
+    # a stale flag (an out-of-range x2 GEMM outside any rollout of this agent) does not discard an update on
+    # given tensors
+    cg = _agent(n_envs=64)
+    x3.gemm(torch.full((64, 264), 2.0 ** 17, device="cuda"), x3.pack(torch.ones(264, 264, device="cuda"), prec="x2"))
+    fx_obs, fx_act, fx_lp, _, _, fx_masks, fx_adv, fx_val = batch
+    cg.update(fx_obs, fx_act, fx_lp, fx_masks, fx_adv, fx_val)
+    assert not cg.last_update_discarded and cg.gemm_prec == "x2" and cg.range_redos == 0
