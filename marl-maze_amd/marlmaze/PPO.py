@@ -46,6 +46,14 @@ ROLLOUT_SIDE_STREAM = os.environ.get("MARLMAZE_ROLLOUT_SIDE", "1") != "0"
 # the observations only, and the weights do not change during a rollout): no critic launch and no cross-stream
 # hand-off per step.  MARLMAZE_ROLLOUT_CRITIC=step keeps the per-step form (A/B)
 ROLLOUT_BATCHED_CRITIC = os.environ.get("MARLMAZE_ROLLOUT_CRITIC", "batched") != "step"
+# the update's critic (forward, value loss, backward) on a side stream beside the actor's kernels: the two
+# networks share nothing until the loss values and the optimizer step.  At small minibatches (BASELINE
+# configs[1]: 26,214 samples) the kernels of either network leave most CUs idle, and at the headline's 209,715
+# the critic's kernels still fill the actor's tails: measured (same box, alternating) configs[1] 5.25M ->
+# 5.38M env-steps/s, headline 6.96M -> 7.07M, f16 share 8.76M -> 8.95M.  MARLMAZE_CRITIC_STREAM=on (default)
+# / off / auto (side stream up to CRITIC_STREAM_MAX_SAMPLES samples per minibatch)
+CRITIC_STREAM = os.environ.get("MARLMAZE_CRITIC_STREAM", "on")
+CRITIC_STREAM_MAX_SAMPLES = int(os.environ.get("MARLMAZE_CRITIC_STREAM_MAX", "65536"))
 
 
 def _ppo_loss_fwd(heads, mk, a8, old_logp, adv, clip):
@@ -527,6 +535,11 @@ class PPO:
         M = obs.shape[0]
         a8 = (act if act.dtype == torch.int8 else act.to(torch.int8)).contiguous()
         mk = _u8(masks)
+        if out is None:
+            out = torch.empty(2, dtype=torch.float32, device=obs.device)
+        side = CRITIC_STREAM == "on" or (CRITIC_STREAM == "auto" and M <= CRITIC_STREAM_MAX_SAMPLES)
+        if side:
+            return self._minibatch_grads_two_streams(obs, a8, old_logp, adv, rtg, mk, out)
         with x3.cached_packs():
             # every weight pack of both networks' forward and backward in one launch per precision, and
             # the backwards' bias-gradient and weight-gradient reductions together at their end
@@ -536,13 +549,41 @@ class PPO:
             heads, asaved = self.actor.train_forward(obs.reshape(2 * M, 65))
             coef, ppo_part = _ppo_loss_fwd(heads, mk, a8, old_logp, adv, self.clip)
             dz = _ppo_loss_bwd(heads, mk, a8, coef, self._one)
-            if out is None:
-                out = torch.empty(2, dtype=torch.float32, device=obs.device)
             update.losses_final(ppo_part, mse_part, M, out)
             with x3.deferred():
                 self.actor.train_backward(asaved, dz)
                 self.critic.train_backward(csaved, dv)
         return out[0], out[1]
+
+    def _minibatch_grads_two_streams(self, obs, a8, old_logp, adv, rtg, mk, out):
+        """minibatch_grads with the critic's forward, value loss and backward on a side stream, beside the
+        actor's (the same kernels and arithmetic: the same results bit for bit).  The side stream waits for
+        the weight packs; the main stream waits for the critic before the loss values and the optimizer."""
+        M = obs.shape[0]
+        cur = torch.cuda.current_stream(obs.device)
+        side = self._critic_update_stream()
+        with x3.cached_packs():
+            x3.pack_many(self.critic.pack_specs() + self.actor.pack_specs())
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                V, csaved = self.critic.train_forward(obs.reshape(M, -1))
+                mse_part, dv = update.mse_loss(V, rtg)
+                with x3.deferred():
+                    self.critic.train_backward(csaved, dv)
+            heads, asaved = self.actor.train_forward(obs.reshape(2 * M, 65))
+            coef, ppo_part = _ppo_loss_fwd(heads, mk, a8, old_logp, adv, self.clip)
+            dz = _ppo_loss_bwd(heads, mk, a8, coef, self._one)
+            with x3.deferred():
+                self.actor.train_backward(asaved, dz)
+            cur.wait_stream(side)
+            mse_part.record_stream(cur)  # (allocated on the side stream, read on this one)
+            update.losses_final(ppo_part, mse_part, M, out)
+        return out[0], out[1]
+
+    def _critic_update_stream(self):
+        if getattr(self, "_cupd_stream", None) is None:
+            self._cupd_stream = torch.cuda.Stream(device=self.device)
+        return self._cupd_stream
 
     def _minibatch_grads_host(self, obs, act, old_logp, adv, rtg, masks):
         """The CPU torch form (autograd, the reference's formulas)."""

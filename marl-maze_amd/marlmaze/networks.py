@@ -280,7 +280,48 @@ def _mlp_fwd(h0, ws, bs, prec, need_bits, act16=False):
     return hs, bits
 
 
-def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None):
+# the actor backward's weight gradients on a side stream (MARLMAZE_WGRAD_STREAM=1; default off): a layer's
+# weight gradient and its input-gradient GEMM read the same dY and nothing else in common, so the weight
+# gradients (and the heads') could run beside the input-gradient chain and the front-end backward.  Measured
+# slower (same box, alternating): headline 7.11M -> 6.84-6.98M env-steps/s, configs[1] 5.37M -> 5.01M --
+# both sides are grids of one large-LDS workgroup per CU (k_wgrad_dma 156 KB, k_bres 152 KB), so sharing the
+# CUs splits each into two rounds instead of overlapping them
+WGRAD_STREAM = os.environ.get("MARLMAZE_WGRAD_STREAM", "0") == "1"
+_WSTREAMS = {}
+
+
+def wgrad_stream(device):
+    """The side stream of the weight gradients (one per device)."""
+    st = _WSTREAMS.get(device)
+    if st is None:
+        st = _WSTREAMS[device] = torch.cuda.Stream(device=device)
+    return st
+
+
+class _OnSide:
+    """with _OnSide(side, *tensors): the block's launches go to ``side`` after everything queued so far on the
+    current stream, and the tensors (made on the current stream) are not reused by the caching allocator
+    before the side stream's work on them is done.  side None: the current stream, nothing else."""
+
+    def __init__(self, side, *tensors):
+        self.side, self.tensors = side, tensors
+
+    def __enter__(self):
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream(self.side.device))
+            for t in self.tensors:
+                t.record_stream(self.side)
+            self.ctx = torch.cuda.stream(self.side)
+            self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.side is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
+def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None, wside=None):
     """Backward through the ReLU layers given dY of the last one (already through
     its ReLU) and that dY's per-tile column sums cs (None: sum dY itself).
     outs: destinations [dW0, db0, dW1, db1, ...] (or None: allocated).
@@ -297,7 +338,8 @@ def _mlp_bwd(ctx_bits, hs, ws, dy, cs, prec, need_dx, outs=None):
     dx = None
     for l in range(L - 1, -1, -1):
         o_w, o_b = (outs[2 * l], outs[2 * l + 1]) if outs is not None else (None, None)
-        grads[2 * l] = _wgrad(dy, hs[l], prec, out=o_w)
+        with _OnSide(wside, dy, hs[l]):
+            grads[2 * l] = _wgrad(dy, hs[l], prec, out=o_w)
         assert cs is not None or not g16, "an fp16 dY comes with its column sums"
         grads[2 * l + 1] = x3.colsum(dy if cs is None else cs, out=o_b)
         wt = x3.pack(ws[l], trans=True, prec=prec)
@@ -350,12 +392,13 @@ def _heads_fwd(h, wh, bh):
     return out
 
 
-def _heads_bwd(dz, h, wh, bits, out_w=None, out_b=None, oscale=None):
+def _heads_bwd(dz, h, wh, bits, out_w=None, out_b=None, oscale=None, wside=None):
     """The heads' backward: (dY through the last ReLU, its tile column sums, dWh, dbh).  oscale: dY
-    stored fp16 pre-scaled (fp16(dY oscale), see _g16)."""
+    stored fp16 pre-scaled (fp16(dY oscale), see _g16).  wside: as _mlp_bwd's."""
     from . import x3
 
-    dwh = _wgrad(dz, h, "x3", out=out_w)
+    with _OnSide(wside, dz, h):
+        dwh = _wgrad(dz, h, "x3", out=out_w)
     dbh = x3.colsum(dz, out=out_b)
     dy, cs = x3.heads_bwd(dz, wh, bits, oscale=oscale)  # (dz Wh) * (h > 0)
     return dy, cs, dwh, dbh
@@ -631,8 +674,15 @@ class Actor(nn.Module):
         gb = self._adjacent(_grad_of(self.move_head.bias), _grad_of(self.mark_head.bias))
         params = self._mlp_params()
         g16 = _g16(self.gemm_prec, hs, params[0::2], True)
+        from . import x3
+
+        # the weight gradients beside the input-gradient chain (only their row-slice partials are launched in
+        # a deferred() scope, so the side stream never writes a .grad; the sums run after the join below)
+        wside = wgrad_stream(dz.device) if (WGRAD_STREAM and dz.is_cuda and x3._DEFER) else None
+        cur = torch.cuda.current_stream(dz.device) if wside is not None else None
         dy, cs, dwh, dbh = _heads_bwd(dz.contiguous(), hs[L], w, bits[L - 1], out_w=gw, out_b=gb,
-                                      oscale=_grad_scale(dz.shape[0], self.gemm_prec) if g16 else None)
+                                      oscale=_grad_scale(dz.shape[0], self.gemm_prec) if g16 else None,
+                                      wside=wside if gw is not None else None)
         if gw is None:
             self.move_head.weight.grad.copy_(dwh[:5])
             self.mark_head.weight.grad.copy_(dwh[5:])
@@ -641,9 +691,11 @@ class Actor(nn.Module):
             self.mark_head.bias.grad.copy_(dbh[5:])
         params = self._mlp_params()
         dh0, _ = _mlp_bwd(bits, hs, params[0::2], dy, cs, self.gemm_prec, True,
-                          outs=[_grad_of(p) for p in params])
+                          outs=[_grad_of(p) for p in params], wside=wside)
         _front_bwd_to(ws, x, self.projection.parity_mode, dh0,
                       [_grad_of(p) for p in front_params(self.projection, self.attention)])
+        if wside is not None:
+            cur.wait_stream(wside)  # the partials are written before the deferred sums read them
 
 
 def _front_fwd_algo(B):

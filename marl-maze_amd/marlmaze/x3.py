@@ -169,6 +169,10 @@ class deferred:
 
     def flush(self):
         L, st = _lib.lib(), _lib.stream_ptr()
+        cur = torch.cuda.current_stream(self.keep[0].device) if self.keep and self.keep[0].is_cuda else None
+        for t in self.keep:  # partials a side stream made (networks.wgrad_stream): read here, on this stream
+            if cur is not None:
+                t.record_stream(cur)
         for i in range(0, len(self.cols), 16):
             chunk = self.cols[i:i + 16]
             arr = (_lib.ColsumSeg * len(chunk))(*chunk)

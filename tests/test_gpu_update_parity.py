@@ -565,3 +565,28 @@ def test_rollout_range_flag_discards_the_batch():
     fx_obs, fx_act, fx_lp, _, _, fx_masks, fx_adv, fx_val = batch
     cg.update(fx_obs, fx_act, fx_lp, fx_masks, fx_adv, fx_val)
     assert not cg.last_update_discarded and cg.gemm_prec == "x2" and cg.range_redos == 0
+
+
+@pytest.mark.parametrize("S", [3000, 26214, 100000])
+def test_side_streams_update_is_bit_identical(golden, monkeypatch, S):
+    """The update's critic on a side stream beside the actor (PPO.CRITIC_STREAM) and the actor's weight
+    gradients on another beside its input-gradient chain (networks.WGRAD_STREAM) run the same kernels on the
+    same inputs: every gradient, both losses and the Adam step equal the one-stream update bit for bit
+    (main.py's 3,000-sample minibatch, configs[1]'s 26,214, and a large one)."""
+    from marlmaze import PPO as ppo_mod
+    from marlmaze import networks as nets_mod
+
+    fx = golden("nets")
+    batch = [t.cuda() for t in _minibatch(fx, S, noise=0.05)]
+    res = []
+    for mode in ("off", "on"):
+        monkeypatch.setattr(ppo_mod, "CRITIC_STREAM", mode)
+        monkeypatch.setattr(nets_mod, "WGRAD_STREAM", mode == "on")
+        actor, critic = _oracle_nets(fx)
+        ag = _agent(n_envs=64)
+        _to_gpu(ag, actor, critic)
+        out = ag.minibatch_step(*batch)
+        torch.cuda.synchronize()
+        res.append((torch.stack(out).cpu(), ag.flat.data.clone(), ag.flat.grad.clone()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
