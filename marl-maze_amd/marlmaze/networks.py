@@ -286,7 +286,9 @@ def _mlp_fwd(h0, ws, bs, prec, need_bits, act16=False):
 # slower (same box, alternating): headline 7.11M -> 6.84-6.98M env-steps/s, configs[1] 5.37M -> 5.01M --
 # both sides are grids of one large-LDS workgroup per CU (k_wgrad_dma 156 KB, k_bres 152 KB), so sharing the
 # CUs splits each into two rounds instead of overlapping them
-WGRAD_STREAM = os.environ.get("MARLMAZE_WGRAD_STREAM", "0") == "1"
+# "heads": only the heads' weight gradient (x3, 6 x 264) beside the heads' backward and the trunk
+WGRAD_STREAM = os.environ.get("MARLMAZE_WGRAD_STREAM", "0")
+WGRAD_STREAM = False if WGRAD_STREAM == "0" else ("heads" if WGRAD_STREAM == "heads" else True)
 _WSTREAMS = {}
 
 
@@ -691,7 +693,7 @@ class Actor(nn.Module):
             self.mark_head.bias.grad.copy_(dbh[5:])
         params = self._mlp_params()
         dh0, _ = _mlp_bwd(bits, hs, params[0::2], dy, cs, self.gemm_prec, True,
-                          outs=[_grad_of(p) for p in params], wside=wside)
+                          outs=[_grad_of(p) for p in params], wside=wside if WGRAD_STREAM is True else None)
         _front_bwd_to(ws, x, self.projection.parity_mode, dh0,
                       [_grad_of(p) for p in front_params(self.projection, self.attention)])
         if wside is not None:
