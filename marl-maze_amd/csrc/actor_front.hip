@@ -350,13 +350,52 @@ __device__ __forceinline__ void stage_tables(const float* __restrict__ ws, float
     }
 }
 
+// k rows of the forward's K image, padded from 10 to kKqP = 12 floats (48 bytes): every row starts
+// 16-byte aligned, so a q.k_j reads one row as two ds_read_b128 + one ds_read_b64 (10 LDS cycles per
+// wave) -- at the unpadded 40-byte pitch every other row is only 8-byte aligned and the compiler reads
+// all rows as ds_read2_b64 pairs (20 cycles).  The forward is bound by LDS cycles (per wave-iteration
+// of two samples ~1,280 LDS cycles against ~650 VALU instructions), so this is the K share of that.
+#ifndef FRONT_FWD_KPITCH
+#define FRONT_FWD_KPITCH 12
+#endif
+constexpr int kKqP = FRONT_FWD_KPITCH;
+static_assert(kKqP == 10 || kKqP == 12, "FRONT_FWD_KPITCH is 10 or 12");
+__device__ __forceinline__ void store_krow(float* kr, const float* k) {
+    if constexpr (kKqP == 12) {
+        *reinterpret_cast<float4*>(kr) = make_float4(k[0], k[1], k[2], k[3]);
+        *reinterpret_cast<float4*>(kr + 4) = make_float4(k[4], k[5], k[6], k[7]);
+        *reinterpret_cast<float2*>(kr + 8) = make_float2(k[8], k[9]);
+    } else {
+#pragma unroll
+        for (int a = 0; a < kKq; a += 2) *reinterpret_cast<float2*>(kr + a) = make_float2(k[a], k[a + 1]);
+    }
+}
+// q . k_j: the same packed-pair order as dot4<10> (pairs (0,1) .. (8,9) into one f32x2 accumulator), so
+// h is bit-identical at either pitch
+__device__ __forceinline__ float dot_krow(const float* q, const float* __restrict__ kr) {
+    if constexpr (kKq == 10 && kKqP == 12) {
+        const float4 v0 = *reinterpret_cast<const float4*>(kr);
+        const float4 v1 = *reinterpret_cast<const float4*>(kr + 4);
+        const float2 v2 = *reinterpret_cast<const float2*>(kr + 8);
+        f32x2 acc = {0.f, 0.f};
+        acc = __builtin_elementwise_fma(f32x2{q[0], q[1]}, f32x2{v0.x, v0.y}, acc);
+        acc = __builtin_elementwise_fma(f32x2{q[2], q[3]}, f32x2{v0.z, v0.w}, acc);
+        acc = __builtin_elementwise_fma(f32x2{q[4], q[5]}, f32x2{v1.x, v1.y}, acc);
+        acc = __builtin_elementwise_fma(f32x2{q[6], q[7]}, f32x2{v1.z, v1.w}, acc);
+        acc = __builtin_elementwise_fma(f32x2{q[8], q[9]}, f32x2{v2.x, v2.y}, acc);
+        return acc.x + acc.y;
+    } else {
+        return dot4<kKq>(q, kr);
+    }
+}
+
 // H16: h stored as fp16 (the fp16 networks' update: their first trunk GEMM and its weight gradient round h to
 // fp16 anyway), rounded to nearest from the same fp32 values
 template <bool H16 = false>
 __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws, const float* __restrict__ x,
                                                    int ldx, int B, int parity, void* __restrict__ hv) {
     __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
-    __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKq];
+    __shared__ __attribute__((aligned(16))) float Ks[kFwdRows][kTok][kKqP];
     __shared__ __attribute__((aligned(16))) float Vs[kFwdRows][kTok][kEmb];
     stage_tables(ws, tab);
     __syncthreads();
@@ -376,10 +415,8 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
             affine4t<kQkv>(ti, ti + kQkv * kPin, xv, o);
 #pragma unroll
             for (int a = 0; a < kKq; a++) q[a] = o[a];
-            // 8- and 16-byte LDS writes (rows of 40 and 80 bytes) instead of 30 4-byte ones
-#pragma unroll
-            for (int a = 0; a < kKq; a += 2)
-                *reinterpret_cast<float2*>(&Ks[g][i][a]) = make_float2(o[kKq + a], o[kKq + a + 1]);
+            // 16- and 8-byte LDS writes (k rows padded to 48 bytes, v rows of 80) instead of 30 4-byte ones
+            store_krow(&Ks[g][i][0], o + kKq);
 #pragma unroll
             for (int c = 0; c < kEmb; c += 4)
                 *reinterpret_cast<float4*>(&Vs[g][i][c]) =
@@ -391,7 +428,7 @@ __global__ __launch_bounds__(256) void k_front_fwd(const float* __restrict__ ws,
             float mx = -INFINITY;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                s[j] = fwd_score(dot4<kKq>(q, Ks[g][j]));
+                s[j] = fwd_score(dot_krow(q, Ks[g][j]));
                 mx = fmaxf(mx, s[j]);
             }
             float sum0 = 0.f, sum1 = 0.f;  // even / odd j: two short chains (the backward recomputes the same way)
@@ -446,7 +483,7 @@ constexpr int kF2Rows = 256 / kF2Lanes;     // 16 samples per workgroup iteratio
 __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__ ws, const float* __restrict__ x,
                                                        int ldx, int B, int parity, float* __restrict__ h) {
     __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
-    __shared__ __attribute__((aligned(16))) float Ks[kF2Rows][kTok][kKq];
+    __shared__ __attribute__((aligned(16))) float Ks[kF2Rows][kTok][kKqP];
     __shared__ __attribute__((aligned(16))) float Vs[kF2Rows][kTok][kEmb];
     stage_tables(ws, tab);
     __syncthreads();
@@ -474,9 +511,7 @@ __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__
             affine4t<kQkv>(ta, ta + kQkv * kPin, xa, o);
 #pragma unroll
             for (int a = 0; a < kKq; a++) qa[a] = o[a];
-#pragma unroll
-            for (int a = 0; a < kKq; a += 2)
-                *reinterpret_cast<float2*>(&Ks[g][i0][a]) = make_float2(o[kKq + a], o[kKq + a + 1]);
+            store_krow(&Ks[g][i0][0], o + kKq);
 #pragma unroll
             for (int c = 0; c < kEmb; c += 4)
                 *reinterpret_cast<float4*>(&Vs[g][i0][c]) =
@@ -485,9 +520,7 @@ __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__
 #pragma unroll
             for (int a = 0; a < kKq; a++) qb[a] = o[a];
             if (own1) {
-#pragma unroll
-                for (int a = 0; a < kKq; a += 2)
-                    *reinterpret_cast<float2*>(&Ks[g][i1][a]) = make_float2(o[kKq + a], o[kKq + a + 1]);
+                store_krow(&Ks[g][i1][0], o + kKq);
 #pragma unroll
                 for (int c = 0; c < kEmb; c += 4)
                     *reinterpret_cast<float4*>(&Vs[g][i1][c]) =
@@ -500,8 +533,8 @@ __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__
             float mxa = -INFINITY, mxb = -INFINITY;
 #pragma unroll
             for (int j = 0; j < kTok; j++) {
-                sa[j] = fwd_score(dot4<kKq>(qa, Ks[g][j]));
-                sb[j] = fwd_score(dot4<kKq>(qb, Ks[g][j]));
+                sa[j] = fwd_score(dot_krow(qa, Ks[g][j]));
+                sb[j] = fwd_score(dot_krow(qb, Ks[g][j]));
                 mxa = fmaxf(mxa, sa[j]);
                 mxb = fmaxf(mxb, sb[j]);
             }
