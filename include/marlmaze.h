@@ -364,6 +364,11 @@ int mm_heads_fwd_h16(const void* h, int ldh, int K, const float* w, const float*
  * values): the f16 networks' update, whose first GEMM (fp16 A at K = 460: the
  * streaming kernel) and its weight gradient round h to fp16 anyway. */
 int mm_actor_front_fwd_h16(const float* ws, const float* x, int ldx, int B, int parity, void* h, void* stream);
+/* mm_actor_front_fwd_h16 with the kernel chosen by `algo` (MM_FRONT_FWD_ROW1 or
+ * MM_FRONT_FWD_MFMA, defined below): h16 is the round to nearest of that
+ * kernel's fp32 h. */
+int mm_actor_front_fwd_h16_ex(const float* ws, const float* x, int ldx, int B, int parity, void* h, int algo,
+                              void* stream);
 
 /* The actor trunk's three ReLU layers (networks.py:35-36) in one launch, for
  * the rollout's small row counts (BASELINE configs[1]: 8,192 rows per step,
@@ -514,12 +519,16 @@ int mm_actor_front_prep(const float* const* wproj, const float* const* bproj, co
                         const float* wv, float* ws, void* stream);
 int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h, void* stream);
 
-/* mm_actor_front_fwd with the kernel chosen by `algo` (bit-identical h):
+/* mm_actor_front_fwd with the kernel chosen by `algo`:
  * MM_FRONT_FWD_ROW1 (mm_actor_front_fwd's): one query row per lane;
  * MM_FRONT_FWD_ROW2: two query rows per lane, each k_j / v_j LDS read feeding
- * both (half the K/V LDS reads per sample). */
+ * both (half the K/V LDS reads per sample; bit-identical to ROW1);
+ * MM_FRONT_FWD_MFMA: the two attention products on the fp32 MFMA (fp32 fmaf
+ * chains in another summation order: within fp32 rounding of ROW1, not
+ * bit-identical to it). */
 #define MM_FRONT_FWD_ROW1 0
 #define MM_FRONT_FWD_ROW2 1
+#define MM_FRONT_FWD_MFMA 2
 int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, int B, int parity, float* h, int algo,
                           void* stream);
 

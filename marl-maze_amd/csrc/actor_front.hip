@@ -165,8 +165,9 @@ __device__ __forceinline__ void affine4(const float* __restrict__ M, const float
 
 // affine4 over a column-major (transposed) [4][R] matrix: rows r, r + 1 of each column are adjacent, so
 // every step is one packed FMA on aligned pairs (the [R][4] form needs two moves per packed FMA to pair
-// up rows).  Same per-element order as affine4 (mul, three fmas, + c): bit-identical results.
-template <int R>
+// up rows).  Same per-element order as affine4 (mul, three fmas, + c): bit-identical results.  Rows
+// [LO, HI) only when given (multiples of 4).
+template <int R, int LO = 0, int HI = R>
 __device__ __forceinline__ void affine4t(const float* __restrict__ MT, const float* __restrict__ c, float4 xv,
                                          float o[R]) {
     const f32x2 x0 = {xv.x, xv.x}, x1 = {xv.y, xv.y}, x2 = {xv.z, xv.z}, x3 = {xv.w, xv.w};
@@ -176,7 +177,7 @@ __device__ __forceinline__ void affine4t(const float* __restrict__ MT, const flo
     const float4* m3 = reinterpret_cast<const float4*>(MT + 3 * R);
     const float4* c4 = reinterpret_cast<const float4*>(c);
 #pragma unroll
-    for (int r4 = 0; r4 < R / 4; r4++) {
+    for (int r4 = LO / 4; r4 < HI / 4; r4++) {
         const float4 a = m0[r4], b = m1[r4], d = m2[r4], e = m3[r4], cv = c4[r4];
         f32x2 lo = f32x2{a.x, a.y} * x0, hi = f32x2{a.z, a.w} * x0;
         lo = __builtin_elementwise_fma(f32x2{b.x, b.y}, x1, lo);
@@ -589,6 +590,245 @@ __global__ __launch_bounds__(256, 2) void k_front_fwd2(const float* __restrict__
                         make_float4(t[c] + ob[c], t[c + 1] + ob[c + 1], t[c + 2] + ob[c + 2], t[c + 3] + ob[c + 3]);
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// forward on the fp32 MFMA (k_front_fwd_mfma)
+// ---------------------------------------------------------------------------
+// k_front_fwd spends its time on LDS cycles, not on arithmetic: every lane
+// reads all 23 k_j / v_j rows of its sample as broadcasts, ~1,100 LDS cycles
+// per wavefront and two samples against ~650 VALU instructions.  Here the two
+// products run on v_mfma_f32_32x32x2_f32 (an exact fp32 fmaf chain per output,
+// no operand split), one sample at a time on the whole wavefront:
+//   S^T   = K Q^T    [j][i], k = a (10: five steps, no padding)
+//   ctx^T = V^T P^T  [c][i], k = j (23 -> 24: twelve steps), accumulated onto t^T
+// Phase 1 is k_front_fwd's (lane = token, the wavefront's two samples in its
+// two halves, folded maps from the staged tables).  The MFMA operands then come
+// from registers: lane half 1 needs the other sample's q / k / t values of its
+// token, one v_permlane32_swap per register pair (lanes 32-63 of the first
+// operand trade with lanes 0-31 of the second), so sample 0's k-step e pairs
+// a = 5 + e (lanes 0-31) with a = e (lanes 32-63), and the same for sample 1.
+// The S^T C tile (lane l: column i = l & 31, register r: row j = (r & 3) +
+// 8 (r >> 2) + 4 (l >> 5)) is the B operand of the second product as it stands
+// (k-step r, k-lane l >> 5 = row j of register r); its A operand V^T reads
+// v_j[c] from LDS (V image [32][20] per sample, rows 23-31 zero) with lanes
+// c = l & 31 on consecutive words.  The result's lane holds token i's
+// columns c = 4 (l >> 5) + 0..3, 8 + .., 16 + .. (lanes 0-31): 16-byte stores.
+// LDS per workgroup: the tables (27.6 KB) and eight V images (20 KB), three
+// workgroups per CU.  The softmax is k_front_fwd's (fwd_score / fwd_exp /
+// fwd_rcp), over the 8 + 4 register rows of the lane and its partner lane.
+constexpr int kFMRows = 8;  // samples per workgroup iteration: two per wavefront
+// waves per SIMD the register budget is cut for (2: 256 VGPRs, 222 used, two workgroups per CU; 3: 168,
+// with spills, three per CU as the LDS allows)
+#ifndef FRONT_FM_WAVES
+#define FRONT_FM_WAVES 3
+#endif
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+__device__ __forceinline__ f32x16_t mfma32(float a, float b, f32x16_t c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// v_permlane32_swap(a, b): s0 = {a of lanes 0-31, b of lanes 0-31}, s1 = {a of lanes 32-63, b of lanes 32-63}
+// -- with the wavefront's sample 0 in lanes 0-31 and sample 1 in lanes 32-63, s0 holds sample 0's a (low
+// lanes) and b (high lanes), s1 sample 1's
+__device__ __forceinline__ void swap32(float a, float b, float& s0, float& s1) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    s0 = __uint_as_float(r[0]);
+    s1 = __uint_as_float(r[1]);
+}
+
+// 1 (default): the wavefront's two samples' MFMA chains interleaved; 0: one after the other
+#ifndef FRONT_FM_ILP
+#define FRONT_FM_ILP 1
+#endif
+
+// softmax over the rows j of the S^T tile's column i: registers r < 12 of both lane halves (j = 23, register
+// 11 of the high half, and j >= 24 are padding); p = P^T's registers
+__device__ __forceinline__ void fm_softmax(f32x16_t& S, int hh, float (&p)[12]) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+        S[r] = fwd_score(S[r]);
+        if (r < 11 || hh == 0) mx = fmaxf(mx, S[r]);
+    }
+    float m0, m1;
+    swap32(mx, mx, m0, m1);
+    mx = fmaxf(m0, m1);
+    float sum0 = 0.f, sum1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+        p[r] = (r < 11 || hh == 0) ? fwd_exp(S[r], mx) : 0.f;
+        if (r & 1) sum1 += p[r];
+        else sum0 += p[r];
+    }
+    float s0, s1;
+    swap32(sum0 + sum1, sum0 + sum1, s0, s1);
+    const float inv = fwd_rcp(s0 + s1);
+#pragma unroll
+    for (int r = 0; r < 12; r++) p[r] *= inv;
+}
+
+// h row `row`, token tok: this lane's column quads 4 hh, 8 + 4 hh (and 16 on lanes 0-31) of ctx^T + t^T
+template <bool H16>
+__device__ __forceinline__ void fm_store(void* hv, int row, int tok, int hh, const f32x16_t& acc) {
+    if (tok >= kTok) return;
+    const int nq = hh ? 2 : 3;
+    if constexpr (H16) {
+        typedef __attribute__((ext_vector_type(4))) _Float16 h4;
+        _Float16* hr = static_cast<_Float16*>(hv) + (size_t)row * kRowF + tok * kEmb + 4 * hh;
+#pragma unroll
+        for (int m = 0; m < 3; m++)
+            if (m < nq)
+                *reinterpret_cast<h4*>(hr + 8 * m) = h4{(_Float16)acc[4 * m], (_Float16)acc[4 * m + 1],
+                                                       (_Float16)acc[4 * m + 2], (_Float16)acc[4 * m + 3]};
+    } else {
+        float* hr = static_cast<float*>(hv) + (size_t)row * kRowF + tok * kEmb + 4 * hh;
+#pragma unroll
+        for (int m = 0; m < 3; m++)
+            if (m < nq)
+                *reinterpret_cast<float4*>(hr + 8 * m) =
+                    make_float4(acc[4 * m], acc[4 * m + 1], acc[4 * m + 2], acc[4 * m + 3]);
+    }
+}
+
+template <bool H16 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRONT_FM_WAVES))) void k_front_fwd_mfma(const float* __restrict__ ws, const float* __restrict__ x,
+                                                        int ldx, int B, int parity, void* __restrict__ hv) {
+    __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
+    __shared__ __attribute__((aligned(16))) float Vs[kFMRows][32][kEmb];
+    for (int e = threadIdx.x; e < kFMRows * 32 * kEmb; e += 256) (&Vs[0][0][0])[e] = 0.f;
+    stage_tables(ws, tab);
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    const int hh = (threadIdx.x >> 5) & 1;  // lane half: phase 1's sample, the MFMAs' k-lane
+    const int tok = threadIdx.x & 31;       // phase 1's token; the MFMA results' column i
+    const int groups = (B + kFMRows - 1) / kFMRows;
+    for (int grp = blockIdx.x; grp < groups; grp += gridDim.x) {
+        const int row0 = grp * kFMRows + 2 * wave;  // the wavefront's samples row0, row0 + 1
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tok < kTok && row0 + hh < B) xv = xslice(x + (size_t)(row0 + hh) * ldx, tok, parity != 0);
+        // ---- phase 1: q | k | v and t of token tok of sample hh (padding tokens and samples past B: the
+        // maps of token 0 at x = 0, finite values that no stored result depends on) ----
+        // the table address behind an opaque copy: the tables are loop-invariant, and hoisted out of the loop
+        // their 300 words per lane spill
+        // (padding lanes 23-31 read token tok - 16's table: their 16-byte reads then fill the bank quads the
+        // other lanes of their ds_read_b128 lane group leave free -- token 0's, the obvious choice, shares
+        // a quad with token 16 in lane group {4-11, 16-19, 28-31}: 2-way conflicts on every table read)
+        int toff = (tok < kTok ? tok : tok - 16) * kTabF;
+        asm volatile("" : "+v"(toff));
+        const float* tl = tab + toff;
+        float o[kQkv], t[kEmb];
+        // table reads in groups of at most ten 16-byte reads, each group's values consumed before the next is
+        // issued (scheduling barriers): issued all at once, the 75 reads per lane need 300 registers
+#define FM_SB __builtin_amdgcn_sched_barrier(0)
+        affine4t<kQkv, 0, 8>(tl, tl + kQkv * kPin, xv, o);
+        FM_SB;
+        affine4t<kQkv, 8, 16>(tl, tl + kQkv * kPin, xv, o);
+        FM_SB;
+        affine4t<kQkv, 16, 20>(tl, tl + kQkv * kPin, xv, o);
+        // MFMA operands per sample s: q / k at k-step e (a = 5 + e on lanes 0-31, a = e on lanes 32-63) and
+        // t in the C layout of ctx^T (register 4 m + u: c = 8 m + 4 hh + u for m < 2, 16 + u for m = 2 on
+        // lanes 0-31)
+        float qs[2][5], ks[2][5], ts[2][12];
+#pragma unroll
+        for (int e = 0; e < 5; e++) {
+            swap32(o[5 + e], o[e], qs[0][e], qs[1][e]);
+            swap32(o[kKq + 5 + e], o[kKq + e], ks[0][e], ks[1][e]);
+        }
+        FM_SB;
+        affine4t<kQkv, 20, 28>(tl, tl + kQkv * kPin, xv, o);
+        FM_SB;
+        affine4t<kQkv, 28, 36>(tl, tl + kQkv * kPin, xv, o);
+        FM_SB;
+        affine4t<kQkv, 36, 40>(tl, tl + kQkv * kPin, xv, o);
+        wave_sync();  // the previous iteration's V readers (this wavefront) are done
+        if (tok < kTok) {
+            float4* vr = reinterpret_cast<float4*>(&Vs[2 * wave + hh][tok][0]);
+#pragma unroll
+            for (int c = 0; c < kEmb / 4; c++)
+                vr[c] = make_float4(o[2 * kKq + 4 * c], o[2 * kKq + 4 * c + 1], o[2 * kKq + 4 * c + 2],
+                                    o[2 * kKq + 4 * c + 3]);
+        }
+        FM_SB;
+        const float* tt = tl + kQkv * (kPin + 1);
+        affine4t<kEmb, 0, 8>(tt, tt + kEmb * kPin, xv, t);
+        FM_SB;
+        affine4t<kEmb, 8, 16>(tt, tt + kEmb * kPin, xv, t);
+        FM_SB;
+        affine4t<kEmb, 16, 20>(tt, tt + kEmb * kPin, xv, t);
+#undef FM_SB
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) swap32(t[8 * m + u], t[8 * m + 4 + u], ts[0][4 * m + u], ts[1][4 * m + u]);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            float dummy;
+            swap32(t[16 + u], t[16 + u], dummy, ts[1][8 + u]);
+            ts[0][8 + u] = t[16 + u];
+        }
+        wave_sync();  // the V images are written
+#if FRONT_FM_ILP
+        // both samples' chains side by side (independent MFMA accumulators and softmax chains: each wave keeps
+        // its own matrix pipe and VALU busy while the other chain waits); a sample past B is computed on the
+        // finite phase-1 values and not stored
+        if (row0 < B) {  // wavefront-uniform
+            f32x16_t S[2] = {{}, {}};
+#pragma unroll
+            for (int e = 0; e < 5; e++) {
+                S[0] = mfma32(ks[0][e], qs[0][e], S[0]);
+                S[1] = mfma32(ks[1][e], qs[1][e], S[1]);
+            }
+            float p[2][12];
+#pragma unroll
+            for (int s = 0; s < 2; s++) fm_softmax(S[s], hh, p[s]);
+            f32x16_t acc[2] = {{}, {}};
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int r = 0; r < 12; r++) acc[s][r] = ts[s][r];
+            const float* vb0 = &Vs[2 * wave][0][0] + tok;
+#pragma unroll
+            for (int r = 0; r < 12; r++) {
+                const int j = (r & 3) + 8 * (r >> 2) + 4 * hh;
+                acc[0] = mfma32(vb0[j * kEmb], p[0][r], acc[0]);
+                acc[1] = mfma32(vb0[32 * kEmb + j * kEmb], p[1][r], acc[1]);
+            }
+            fm_store<H16>(hv, row0, tok, hh, acc[0]);
+            if (row0 + 1 < B) fm_store<H16>(hv, row0 + 1, tok, hh, acc[1]);
+        }
+#else
+        // one sample at a time (a rolled loop: the second sample's operands move into the first's registers at
+        // the end of the first pass; unrolled, the two chains interleave and spill)
+#pragma unroll 1
+        for (int s = 0; s < 2; s++) {
+            const int row = row0 + s;
+            if (row >= B) break;  // wavefront-uniform
+            f32x16_t S = {};
+#pragma unroll
+            for (int e = 0; e < 5; e++) S = mfma32(ks[0][e], qs[0][e], S);
+            float p[12];
+            fm_softmax(S, hh, p);
+            // ctx^T + t^T: A = V^T (v_j[c], c = l & 31: words past c = 19 are the next row's, finite, and only
+            // reach rows c >= 20 of the result), B = P^T (register r)
+            const float* vb = &Vs[2 * wave + s][0][0] + tok;
+            f32x16_t acc = {};
+#pragma unroll
+            for (int r = 0; r < 12; r++) acc[r] = ts[0][r];
+#pragma unroll
+            for (int r = 0; r < 12; r++) {
+                const int j = (r & 3) + 8 * (r >> 2) + 4 * hh;
+                acc = mfma32(vb[j * kEmb], p[r], acc);
+            }
+            fm_store<H16>(hv, row, tok, hh, acc);
+#pragma unroll
+            for (int e = 0; e < 5; e++) qs[0][e] = qs[1][e], ks[0][e] = ks[1][e];
+#pragma unroll
+            for (int r = 0; r < 12; r++) ts[0][r] = ts[1][r];
+        }
+#endif
     }
 }
 
@@ -1505,9 +1745,15 @@ extern "C" int mm_actor_front_prep(const float* const* wproj, const float* const
 extern "C" int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, int B, int parity, float* h,
                                      int algo, void* stream) {
     if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM) return MM_E_ARG;
-    if (algo != MM_FRONT_FWD_ROW1 && algo != MM_FRONT_FWD_ROW2) return MM_E_ARG;
+    if (algo != MM_FRONT_FWD_ROW1 && algo != MM_FRONT_FWD_ROW2 && algo != MM_FRONT_FWD_MFMA) return MM_E_ARG;
     if (B == 0) return 0;
-    if (algo == MM_FRONT_FWD_ROW2) {
+    if (algo == MM_FRONT_FWD_MFMA) {
+        const int groups = (B + kFMRows - 1) / kFMRows;
+        const int cap = FRONT_FM_WAVES * cu_count();  // workgroups per CU = waves per SIMD (48 KB of LDS each)
+        const int grid = groups < cap ? groups : cap;
+        hipLaunchKernelGGL(k_front_fwd_mfma<false>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B,
+                           parity, (void*)h);
+    } else if (algo == MM_FRONT_FWD_ROW2) {
         const int groups = (B + kF2Rows - 1) / kF2Rows;
         const int grid = groups < 2 * cu_count() ? groups : 2 * cu_count();  // two workgroups per CU (72 KB LDS)
         hipLaunchKernelGGL(k_front_fwd2, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
@@ -1520,14 +1766,29 @@ extern "C" int mm_actor_front_fwd_ex(const float* ws, const float* x, int ldx, i
     return (int)hipGetLastError();
 }
 
+extern "C" int mm_actor_front_fwd_h16_ex(const float* ws, const float* x, int ldx, int B, int parity, void* h,
+                                         int algo, void* stream) {
+    if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM || ((uintptr_t)h & 7)) return MM_E_ARG;
+    if (algo != MM_FRONT_FWD_ROW1 && algo != MM_FRONT_FWD_MFMA) return MM_E_ARG;
+    if (B == 0) return 0;
+    if (algo == MM_FRONT_FWD_MFMA) {
+        const int groups = (B + kFMRows - 1) / kFMRows;
+        const int cap = FRONT_FM_WAVES * cu_count();
+        const int grid = groups < cap ? groups : cap;
+        hipLaunchKernelGGL(k_front_fwd_mfma<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B,
+                           parity, h);
+    } else {
+        const int groups = (B + kFwdRows - 1) / kFwdRows;
+        const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();
+        hipLaunchKernelGGL(k_front_fwd<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity,
+                           h);
+    }
+    return (int)hipGetLastError();
+}
+
 extern "C" int mm_actor_front_fwd_h16(const float* ws, const float* x, int ldx, int B, int parity, void* h,
                                       void* stream) {
-    if (!ws || !x || !h || B < 0 || ldx < MM_OBS_DIM || ((uintptr_t)h & 7)) return MM_E_ARG;
-    if (B == 0) return 0;
-    const int groups = (B + kFwdRows - 1) / kFwdRows;
-    const int grid = groups < 3 * cu_count() ? groups : 3 * cu_count();
-    hipLaunchKernelGGL(k_front_fwd<true>, dim3(grid), dim3(256), 0, (hipStream_t)stream, ws, x, ldx, B, parity, h);
-    return (int)hipGetLastError();
+    return mm_actor_front_fwd_h16_ex(ws, x, ldx, B, parity, h, MM_FRONT_FWD_ROW1, stream);
 }
 
 extern "C" int mm_actor_front_fwd(const float* ws, const float* x, int ldx, int B, int parity, float* h,

@@ -46,12 +46,13 @@ EXPORTS = ("mm_version", "mm_env_desc_size", "mm_layout_stride", "mm_env_seed", 
            "mm_gemm_wgrad_partials", "mm_colsum_multi_ws_len", "mm_colsum_multi", "mm_wsum_multi", "mm_critic_value",
            "mm_gemm_range_flag", "mm_gemm_nt_h", "mm_gemm_a16_ok", "mm_gemm_wgrad_h", "mm_gemm_wgrad_partials_h",
            "mm_heads_fwd_h16", "mm_x3_heads_bwd_h16", "mm_trunk3_ok", "mm_trunk3",
-           "mm_trunk3_head_sample_ok", "mm_trunk3_head_sample", "mm_actor_front_fwd_h16")
+           "mm_trunk3_head_sample_ok", "mm_trunk3_head_sample", "mm_actor_front_fwd_h16",
+           "mm_actor_front_fwd_h16_ex")
 VERSION = 307  # mm_version() this binding is written for
 
 PREC_X3, PREC_F16, PREC_X2 = 0, 1, 2  # MM_PREC_*
 FRONT_BWD = {"mfma": 0, "valu": 1}  # MM_FRONT_BWD_*
-FRONT_FWD = {"row1": 0, "row2": 1}  # MM_FRONT_FWD_*
+FRONT_FWD = {"row1": 0, "row2": 1, "mfma": 2}  # MM_FRONT_FWD_*
 GEMM_ALGO = {"auto": 0, "stream": 1}  # MM_GEMM_*
 GEMM_A_F16, GEMM_C_F16, GEMM_B_F16 = 1, 2, 4  # MM_GEMM_A_F16 / _C_F16 / _B_F16
 
@@ -216,6 +217,7 @@ def lib():
                            ("mm_trunk3", [i32, P, i32, i32, i32, P, P, i32, P, P, i32, P, P, i32, P, i32, P]),
                            ("mm_trunk3_head_sample_ok", [i32, i32, i32, i32, i32, i32, i32]),
                            ("mm_actor_front_fwd_h16", [P, P, i32, i32, i32, P, P]),
+                           ("mm_actor_front_fwd_h16_ex", [P, P, i32, i32, i32, P, i32, P]),
                            ("mm_trunk3_head_sample", [i32, P, i32, i32, i32, P, P, i32, P, P, i32, P, P, i32, P, P, P,
                                                       u64, u64, P, P, P, P, P, P, i32, P])):
             if hasattr(L, name):

@@ -96,11 +96,12 @@ def _front_bwd_grid(B, dev):
     if grid < 1:
         raise _lib.MMError(f"mm_actor_front_bwd_grid failed with status {grid}")
     return grid
-# the front-end forward: "row2" (two query rows per lane, half the K/V LDS reads; 16 samples per workgroup, two
-# workgroups per CU) or "row1" (one per lane; 8 samples, three per CU); bit-identical outputs (csrc/actor_front.hip
-# k_front_fwd2 / k_front_fwd).  "auto": row2 up to FRONT_FWD_ROW2_MAX samples (one round of its grid where row1
-# needs two), row1 above
-FRONT_FWD_ALGO = os.environ.get("MARLMAZE_FRONT_FWD", "row1")
+# the front-end forward: "mfma" (default: both attention products on the fp32 MFMA, k_front_fwd_mfma; 13% faster
+# than row1 at 419,430 rows, 4-9% at the rollout's sizes), "row1" (VALU, one query row per lane; 8 samples, three
+# workgroups per CU) or "row2" (two query rows per lane, half the K/V LDS reads; 16 samples per workgroup, two
+# workgroups per CU); row1 and row2 are bit-identical, mfma within fp32 rounding of them (csrc/actor_front.hip).
+# "auto": row2 up to FRONT_FWD_ROW2_MAX samples (one round of its grid where row1 needs two), row1 above
+FRONT_FWD_ALGO = os.environ.get("MARLMAZE_FRONT_FWD", "mfma")
 FRONT_FWD_ROW2_MAX = int(os.environ.get("MARLMAZE_FRONT_FWD_ROW2_MAX", "8192"))
 
 
@@ -730,8 +731,9 @@ def _front_fwd(x, parity, params, h16=False):
     ws = x3.cached_value("front_prep", params, prep)
     if h16:
         h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float16, device=x.device)
-        _lib.check(L.mm_actor_front_fwd_h16(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
-                                            stream), "mm_actor_front_fwd_h16")
+        algo = _lib.FRONT_FWD["mfma" if _front_fwd_algo(B) == "mfma" else "row1"]
+        _lib.check(L.mm_actor_front_fwd_h16_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),
+                                               algo, stream), "mm_actor_front_fwd_h16_ex")
         return ws, h
     h = torch.empty((B, FEATURE_AMOUNT * EMBEDDING_DIM), dtype=torch.float32, device=x.device)
     _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), OBS_SPACE, B, int(parity), _lib.ptr(h),

@@ -250,6 +250,57 @@ def test_front_forward_row2_bit_identical(parity, B):
     assert torch.equal(hs[0][:B], hs[1][:B])
 
 
+@pytest.mark.parametrize("B", [1, 2, 15, 17, 3001, 131072])
+@pytest.mark.parametrize("parity", [True, False])
+def test_front_forward_mfma_vs_fp64(parity, B):
+    """k_front_fwd_mfma (both attention products on the fp32 MFMA, h = t + ctx accumulated in the
+    MFMA) against an fp64 evaluation of the same modules: as close to fp64 as the VALU kernel (within
+    twice its error, or 2e-7 of max|h|), every row written and nothing past B (ragged B: odd counts leave
+    a wavefront's second sample and a workgroup's tail empty; 131,072 rows: the persistent grid's
+    multi-iteration case), and the fp16 form the round to nearest of the fp32 one."""
+    import copy
+    import ctypes
+
+    from marlmaze import _lib
+    from marlmaze.networks import Actor, front_params
+
+    torch.manual_seed(2)
+    actor = Actor([264, 264, 264], parity_mode=parity).cuda()
+    with torch.no_grad():  # non-trivial attention weights
+        for p in actor.parameters():
+            p.mul_(3.0)
+    x = torch.randn(B, 65, device="cuda")
+    params = front_params(actor.projection, actor.attention)
+    L = _lib.lib()
+    ws = torch.empty(L.mm_actor_front_ws_len(), dtype=torch.float32, device="cuda")
+    ptrs = [p.data_ptr() for p in params]
+    wp = (ctypes.c_void_p * 23)(*ptrs[:23])
+    bp = (ctypes.c_void_p * 23)(*ptrs[23:46])
+    s = _lib.stream_ptr()
+    _lib.check(L.mm_actor_front_prep(wp, bp, ptrs[46], ptrs[47], ptrs[48], _lib.ptr(ws), s), "prep")
+    hs = {}
+    for algo in ("row1", "mfma"):
+        h = torch.full((B + 1, 460), float("nan"), device="cuda")  # one guard row past B
+        _lib.check(L.mm_actor_front_fwd_ex(_lib.ptr(ws), _lib.ptr(x), 65, B, int(parity), _lib.ptr(h),
+                                           _lib.FRONT_FWD[algo], s), algo)
+        hs[algo] = h
+    h16 = torch.full((B + 1, 460), float("nan"), device="cuda", dtype=torch.float16)
+    _lib.check(L.mm_actor_front_fwd_h16_ex(_lib.ptr(ws), _lib.ptr(x), 65, B, int(parity), _lib.ptr(h16),
+                                           _lib.FRONT_FWD["mfma"], s), "h16 mfma")
+    torch.cuda.synchronize()
+    h = hs["mfma"]
+    assert torch.isfinite(h[:B]).all()
+    assert torch.isnan(h[B]).all()  # nothing written past B
+    assert torch.isnan(h16[B]).all()
+    assert torch.equal(h16[:B], h[:B].half())
+    a64 = copy.deepcopy(actor).double()
+    with torch.no_grad():
+        h64 = a64.attention(a64.projection(x.double()))
+    e_mfma = (h[:B].double() - h64).abs().max().item()
+    e_row1 = (hs["row1"][:B].double() - h64).abs().max().item()
+    assert e_mfma <= max(2.0 * e_row1, 2e-7 * h64.abs().max().item()), (e_mfma, e_row1)
+
+
 @pytest.mark.parametrize("parity", [True, False])
 def test_front_backward_mfma_vs_fp64(parity, monkeypatch):
     """The front-end's parameter gradients against an fp64 evaluation of the
