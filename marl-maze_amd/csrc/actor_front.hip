@@ -1259,7 +1259,11 @@ __device__ __forceinline__ void ef2_accumulate(const float* sm, const float* __r
                     const int gg = g0 + v;
                     if (gg < nrow) {
                         const float* sg = sm + gg * kStride;
-                        const float4 gv = lds ? *reinterpret_cast<const float4*>(sg + kG + tk * kQkv + r0) : fp[v];
+                        // the G row read unconditionally (for a dctx unit, r0 >= 40, the address is still inside
+                        // the sample's region) and selected by value: as a conditional read, the compiler split
+                        // it into four exec-masked 4-byte reads and moves per unit and sample
+                        const float4 lv = *reinterpret_cast<const float4*>(sg + kG + tk * kQkv + r0);
+                        const float4 gv = lds ? lv : fp[v];
                         const float gr[4] = {gv.x, gv.y, gv.z, gv.w};
                         const float4 xq = *reinterpret_cast<const float4*>(sg + kX + tk * kPin);
                         const f32x2 x01 = {xq.x, xq.y}, x23 = {xq.z, xq.w};
