@@ -643,6 +643,33 @@ __device__ __forceinline__ void swap32(float a, float b, float& s0, float& s1) {
 #ifndef FRONT_FM_ILP
 #define FRONT_FM_ILP 1
 #endif
+// ctx^T = V^T P^T: 1 (default) on the x2 f16 MFMA (v_mfma_f32_32x32x16_f16: hi hi, hi lo, lo hi, two k-steps of
+// 16 rows j: 6 MFMAs of 32 cycles per sample instead of 12 f32 ones of 64), 0 on the fp32 MFMA
+#ifndef FRONT_FM_PV
+#define FRONT_FM_PV 1
+#endif
+static_assert(FRONT_FM_PV == 0 || FRONT_FM_ILP == 1, "the x2 PV product is built in the interleaved form");
+// the V image's scale: v 2^-8 is split, the result scaled back by 2^8 (both exact), so fp16's range covers
+// |v| < 2^24 and the hi plane stays normal down to |v| = 2^-6
+constexpr float kFMVs = 1.f / 256.f, kFMVsInv = 256.f;
+constexpr float kFMLo = 2048.f, kFMLoInv = 1.f / 2048.f;  // x2: x = hi + 2^-11 lo
+typedef _Float16 fm_f16x8 __attribute__((ext_vector_type(8)));
+typedef short fm_s4 __attribute__((ext_vector_type(4)));
+
+// x2 split of two values (x s): hi = RN16(x s), lo = RN16(2^11 (x s - hi)), as x3mlp.hip's pair2
+__device__ __forceinline__ void fm_pair2(float x0, float x1, float s, uint32_t& h, uint32_t& l) {
+    typedef __attribute__((ext_vector_type(2))) _Float16 h2;
+    const f32x2 v = f32x2{x0, x1} * s;
+    const h2 hv = __builtin_convertvector(v, h2);
+    const f32x2 r = (v - __builtin_convertvector(hv, f32x2)) * kFMLo;
+    h = __builtin_bit_cast(uint32_t, hv);
+    l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, h2));
+}
+
+// 4 x 16-bit of a [row][col] LDS image, transposed across each 16-lane group (ds_read_b64_tr_b16)
+__device__ __forceinline__ fm_s4 fm_tr(const uint16_t* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) fm_s4*)(p));
+}
 
 // softmax over the rows j of the S^T tile's column i: registers r < 12 of both lane halves (j = 23, register
 // 11 of the high half, and j >= 24 are padding); p = P^T's registers
@@ -697,8 +724,17 @@ template <bool H16 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRONT_FM_WAVES))) void k_front_fwd_mfma(const float* __restrict__ ws, const float* __restrict__ x,
                                                         int ldx, int B, int parity, void* __restrict__ hv) {
     __shared__ __attribute__((aligned(16))) float tab[kTok * kTabF];
+#if FRONT_FM_PV
+    // V image as x2 fp16 planes [plane][slot][32 rows][20] (rows 23-31 zero), plus a pad: the transposed reads
+    // of columns 20-31 run past a row's end (into the next row, past the last one into the pad) and reach only
+    // rows c >= 20 of the result
+    constexpr int kVpN = kFMRows * 32 * kEmb + 16;
+    __shared__ __attribute__((aligned(16))) uint16_t Vp[2][kVpN];
+    for (int e = threadIdx.x; e < kVpN; e += 256) Vp[0][e] = Vp[1][e] = 0;
+#else
     __shared__ __attribute__((aligned(16))) float Vs[kFMRows][32][kEmb];
     for (int e = threadIdx.x; e < kFMRows * 32 * kEmb; e += 256) (&Vs[0][0][0])[e] = 0.f;
+#endif
     stage_tables(ws, tab);
     __syncthreads();
     const int wave = threadIdx.x >> 6;
@@ -745,11 +781,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRONT_FM_WA
         affine4t<kQkv, 36, 40>(tl, tl + kQkv * kPin, xv, o);
         wave_sync();  // the previous iteration's V readers (this wavefront) are done
         if (tok < kTok) {
+#if FRONT_FM_PV
+            uint32_t vh[kEmb / 2], vl[kEmb / 2];
+#pragma unroll
+            for (int k = 0; k < kEmb / 2; k++) fm_pair2(o[2 * kKq + 2 * k], o[2 * kKq + 2 * k + 1], kFMVs, vh[k], vl[k]);
+            uint2* dh = reinterpret_cast<uint2*>(&Vp[0][((2 * wave + hh) * 32 + tok) * kEmb]);  // 40-byte rows
+            uint2* dl = reinterpret_cast<uint2*>(&Vp[1][((2 * wave + hh) * 32 + tok) * kEmb]);
+#pragma unroll
+            for (int k = 0; k < kEmb / 4; k++) {
+                dh[k] = make_uint2(vh[2 * k], vh[2 * k + 1]);
+                dl[k] = make_uint2(vl[2 * k], vl[2 * k + 1]);
+            }
+#else
             float4* vr = reinterpret_cast<float4*>(&Vs[2 * wave + hh][tok][0]);
 #pragma unroll
             for (int c = 0; c < kEmb / 4; c++)
                 vr[c] = make_float4(o[2 * kKq + 4 * c], o[2 * kKq + 4 * c + 1], o[2 * kKq + 4 * c + 2],
                                     o[2 * kKq + 4 * c + 3]);
+#endif
         }
         FM_SB;
         const float* tt = tl + kQkv * (kPin + 1);
@@ -785,6 +834,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRONT_FM_WA
 #pragma unroll
             for (int s = 0; s < 2; s++) fm_softmax(S[s], hh, p[s]);
             f32x16_t acc[2] = {{}, {}};
+#if FRONT_FM_PV
+            // B = P^T: k-step t takes the S^T registers 8t .. 8t + 7 as they stand (element e of lane half hh is
+            // row j = 16 t + 8 (e >> 2) + 4 hh + (e & 3)), split into the x2 planes; A = V^T: the same rows j of
+            // column c = lane & 31, two transposed 4-row reads per plane (lane 4q + p of a 16-lane group: row q of
+            // the block, columns 4p .. 4p + 3).  acc = t^T 2^-8 + hi hi, accx = hi lo + lo hi; h = 2^8 (acc +
+            // 2^-11 accx)
+            f32x16_t accx[2] = {{}, {}};
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int r = 0; r < 12; r++) acc[s][r] = ts[s][r] * kFMVs;
+            const int lane = threadIdx.x & 63;
+            const int voff = (2 * wave * 32 + 4 * hh + ((lane >> 2) & 3)) * kEmb + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                fm_f16x8 bh[2], bl[2];
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    uint32_t h4[4], l4[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int r = 8 * t + 2 * k;
+                        if (r < 12) fm_pair2(p[s][r], p[s][r + 1], 1.f, h4[k], l4[k]);
+                        else h4[k] = l4[k] = 0u;
+                    }
+                    bh[s] = __builtin_bit_cast(fm_f16x8, make_uint4(h4[0], h4[1], h4[2], h4[3]));
+                    bl[s] = __builtin_bit_cast(fm_f16x8, make_uint4(l4[0], l4[1], l4[2], l4[3]));
+                }
+#pragma unroll
+                for (int s = 0; s < 2; s++) {
+                    const int o0 = voff + (s * 32 + 16 * t) * kEmb;
+                    fm_s4 a0 = fm_tr(&Vp[0][o0]), a1 = fm_tr(&Vp[0][o0 + 8 * kEmb]);
+                    fm_s4 c0 = fm_tr(&Vp[1][o0]), c1 = fm_tr(&Vp[1][o0 + 8 * kEmb]);
+                    const fm_f16x8 ah = __builtin_bit_cast(fm_f16x8, __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    const fm_f16x8 al = __builtin_bit_cast(fm_f16x8, __builtin_shufflevector(c0, c1, 0, 1, 2, 3, 4, 5, 6, 7));
+                    accx[s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl[s], accx[s], 0, 0, 0);
+                    accx[s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh[s], accx[s], 0, 0, 0);
+                    acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh[s], acc[s], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < 2; s++)
+#pragma unroll
+                for (int r = 0; r < 12; r++) acc[s][r] = fmaf(accx[s][r], kFMLoInv, acc[s][r]) * kFMVsInv;
+#else
 #pragma unroll
             for (int s = 0; s < 2; s++)
 #pragma unroll
@@ -796,6 +890,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FRONT_FM_WA
                 acc[0] = mfma32(vb0[j * kEmb], p[0][r], acc[0]);
                 acc[1] = mfma32(vb0[32 * kEmb + j * kEmb], p[1][r], acc[1]);
             }
+#endif
             fm_store<H16>(hv, row0, tok, hh, acc[0]);
             if (row0 + 1 < B) fm_store<H16>(hv, row0 + 1, tok, hh, acc[1]);
         }

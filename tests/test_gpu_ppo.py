@@ -253,9 +253,9 @@ def test_front_forward_row2_bit_identical(parity, B):
 @pytest.mark.parametrize("B", [1, 2, 15, 17, 3001, 131072])
 @pytest.mark.parametrize("parity", [True, False])
 def test_front_forward_mfma_vs_fp64(parity, B):
-    """k_front_fwd_mfma (both attention products on the fp32 MFMA, h = t + ctx accumulated in the
-    MFMA) against an fp64 evaluation of the same modules: as close to fp64 as the VALU kernel (within
-    twice its error, or 2e-7 of max|h|), every row written and nothing past B (ragged B: odd counts leave
+    """k_front_fwd_mfma (S^T on the fp32 MFMA, ctx^T = V^T P^T on the x2 f16 MFMA, h = t + ctx
+    accumulated in the MFMA) against an fp64 evaluation of the same modules: within twice the VALU
+    kernel's error or 1e-6 of max|h| (the x2 GEMMs' bar), every row written and nothing past B (ragged B: odd counts leave
     a wavefront's second sample and a workgroup's tail empty; 131,072 rows: the persistent grid's
     multi-iteration case), and the fp16 form the round to nearest of the fp32 one."""
     import copy
@@ -298,7 +298,9 @@ def test_front_forward_mfma_vs_fp64(parity, B):
         h64 = a64.attention(a64.projection(x.double()))
     e_mfma = (h[:B].double() - h64).abs().max().item()
     e_row1 = (hs["row1"][:B].double() - h64).abs().max().item()
-    assert e_mfma <= max(2.0 * e_row1, 2e-7 * h64.abs().max().item()), (e_mfma, e_row1)
+    # the attention-weighted sum runs on the x2 f16 MFMA (FRONT_FM_PV=1: operands split hi + 2^-11 lo, 2^-22
+    # relative per product): the x2 GEMMs' 1e-6 bar, relative to max|h|
+    assert e_mfma <= max(2.0 * e_row1, 1e-6 * h64.abs().max().item()), (e_mfma, e_row1)
 
 
 @pytest.mark.parametrize("parity", [True, False])
